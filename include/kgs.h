@@ -1,0 +1,130 @@
+/* kgs.h — C-ABI of the MI355X-native KZG grand-sum / grand-product prover (libkgs.so).
+ *
+ * Drop-in boundary for the reference's hot path (xavi-pinsach/kzg-grandsums-study, JavaScript):
+ * the reference has no native layer of its own; its arithmetic runs in the third-party
+ * ffjavascript@0.2.59 / wasmcurves@0.2.1 wasm. Each entry point below names the reference
+ * interface it replaces. Host bindings (N-API addon for the JS modules, ctypes for Python) are
+ * shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Fr / Fq elements: 32 bytes little-endian. "mont" = Montgomery form with R = 2^256 (the
+ *    in-memory form of every ffjavascript field element); "std" = standard form.
+ *  - G1 affine points: 64 bytes x||y, each 32 B LE Montgomery Fq ("LEM", as in .ptau files and in
+ *    ffjavascript `G1.toAffine` output); the point at infinity is 64 zero bytes.
+ *  - Every call returns 0 on success or a negative KGS_E_* code; kgs_last_error() returns the
+ *    message of the last failure on the calling thread. Semantic failures reproduce the
+ *    reference's Error messages verbatim.
+ *  - A context owns one HIP device, one stream, the device-resident SRS (+ MSM window tables) and
+ *    the NTT domain tables. Contexts are not re-entrant.
+ */
+#ifndef KGS_H
+#define KGS_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KGS_OK 0
+#define KGS_E_ARG (-1)             /* bad argument / shape */
+#define KGS_E_HIP (-2)             /* HIP runtime failure */
+#define KGS_E_NOT_WELL_CALC (-3)   /* "The grand-sum polynomial S is not well calculated" (grandsum.js:56)
+                                      "The grand-product polynomial Z is not well calculated" (grandproduct.js:51) */
+#define KGS_E_NOT_DIVISIBLE (-4)   /* "Polynomial is not divisible" (polynomial.js:878) */
+#define KGS_E_DOES_NOT_DIVIDE (-5) /* "Polynomial does not divide" (polynomial.js:847) */
+#define KGS_E_IO (-6)              /* ptau read/write failure (binfileutils / ptau_utils.js:3-24) */
+#define KGS_E_SRS (-7)             /* "The Powers of Tau file is not sufficiently large ..." (prover.js:79-81) */
+
+#define KGS_GRANDSUM 0
+#define KGS_GRANDPRODUCT 1
+
+typedef struct kgs_ctx kgs_ctx_t;
+
+const char* kgs_last_error(void);
+const char* kgs_version(void);
+
+/* Create / destroy a context on HIP device `device`. */
+int kgs_ctx_create(int device, kgs_ctx_t** out);
+void kgs_ctx_destroy(kgs_ctx_t* ctx);
+
+/* Load a .ptau file (binfileutils layout, sections 1-3) and make the first 2^(nbits_max+1) G1
+ * points device-resident, together with the MSM window tables and the NTT tables for domains
+ * up to 2^nbits_max (nbits_max < 0: the file's power). Replaces readBinFile + readPTauHeader +
+ * fd.readToBuffer(section 2) (src/grandsum/mset_eq_kzg_prover.js:15-16,83-85; src/ptau_utils.js:3-24).
+ * Re-loading the same (path, nbits_max) is a no-op (device SRS cache). */
+int kgs_srs_load_ptau(kgs_ctx_t* ctx, const char* path, int nbits_max);
+/* Same from in-memory LEM points (npts >= 2). `power` is the ceremony power to report. */
+int kgs_srs_load_points(kgs_ctx_t* ctx, const uint8_t* g1_lem, uint64_t npts, int power, int nbits_max);
+/* power of the loaded ptau, number of resident points, MSM window c */
+int kgs_srs_info(kgs_ctx_t* ctx, int* power, uint64_t* npts, int* window_c);
+/* Read [tau]_2 (128 B LEM, section 3 offset 128) from a ptau (verifier input,
+ * src/grandsum/mset_eq_kzg_verifier.js:18-19). */
+int kgs_ptau_read_tau_g2(const char* path, uint8_t out128[128]);
+
+/* Write a synthetic ptau (sections 1-3 with the hermez layout; section 3 holds [1]_2 and
+ * [tau]_2 only) for a known tau (32 B LE standard form). G1 powers are generated on the GPU of
+ * `ctx` (or on the CPU if ctx == NULL). */
+int kgs_ptau_write_synthetic(kgs_ctx_t* ctx, const char* path, int power, const uint8_t tau_std[32]);
+
+/* Full prover — replaces mset_eq_kzg_{grandsum,grandproduct}_prover
+ * (src/grandsum/mset_eq_kzg_prover.js:12, src/grandproduct/mset_eq_kzg_prover.js:12).
+ *   kind      KGS_GRANDSUM | KGS_GRANDPRODUCT
+ *   nbits     domain size n = 2^nbits (1 <= nbits <= SRS nbits_max)
+ *   npols     k >= 1 (vector argument when k > 1)
+ *   evals_f/t k host pointers, n x 32 B STANDARD-form evaluations each (the caller's
+ *             Evaluations.eval before prover.js:147-148)
+ *   sel_f/t   n x 32 B MONTGOMERY selector evaluations, or both NULL (unselected; the wrapper
+ *             passes NULL when both are all Fr.one, prover.js:63-68)
+ *   mont_f/t  optional k output pointers (n x 32 B) receiving the Montgomery evaluations that the
+ *             reference writes back into the caller's objects (prover.js:147-148); may be NULL
+ *   commitments_out  (#commitments x 64 B LEM), order:
+ *             grand-sum:     F0,T0,..,F{k-1},T{k-1}, [selF,selT], S, Q, Wxi, Wxiw
+ *             grand-product: F0,T0,..,F{k-1},T{k-1}, [selF,selT], Z, Q, Wxi, Wxiw
+ *   evaluations_out  (#evaluations x 32 B Montgomery), order:
+ *             grand-sum:     f0,t0,..,f{k-1},t{k-1}, [selF,selT], sxiw
+ *             grand-product: f0,..,f{k-1}, [selF,selT], zxiw
+ */
+int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* const* evals_f,
+              const uint8_t* const* evals_t, const uint8_t* sel_f, const uint8_t* sel_t, uint8_t* const* mont_f,
+              uint8_t* const* mont_t, uint8_t* commitments_out, uint8_t* evaluations_out);
+/* Same with device-resident inputs (HIP device pointers on ctx's device). */
+int kgs_prove_device(kgs_ctx_t* ctx, int kind, int nbits, int npols, const void* const* d_evals_f,
+                     const void* const* d_evals_t, const void* d_sel_f, const void* d_sel_t, uint8_t* commitments_out,
+                     uint8_t* evaluations_out);
+/* number of commitments / evaluations a proof of this shape produces */
+int kgs_proof_shape(int kind, int npols, int selected, int* n_commitments, int* n_evaluations);
+
+/* Per-proof timing of the last kgs_prove* call (milliseconds, host wall clock per round). */
+int kgs_last_timing(kgs_ctx_t* ctx, double* rounds_ms, int max_rounds);
+
+/* ---- primitives (host buffers in/out; used by tests and by the bench's roofline legs) ---- */
+/* [ffjs] Fr.batchToMontgomery */
+int kgs_fr_to_mont(kgs_ctx_t* ctx, const uint8_t* in_std, uint8_t* out_mont, uint64_t n);
+/* [ffjs] Fr.fft / Fr.ifft: natural order in and out, size 2^logm, ifft includes 1/m */
+int kgs_ntt(kgs_ctx_t* ctx, const uint8_t* in_mont, uint8_t* out_mont, int logm, int inverse);
+/* [ffjs] G1.multiExpAffine(SRS[0..n), fromMont(scalars)) + toAffine (polynomial.js:1106-1115) */
+int kgs_msm(kgs_ctx_t* ctx, const uint8_t* scalars_mont, uint64_t n, uint8_t out_lem[64]);
+/* ComputeSGrandSumPolynomial / ComputeZGrandProductPolynomial evaluations before the ifft
+ * (grandsum.js:6-57, grandproduct.js:6-52): out = S (or Z) evaluations, natural order */
+int kgs_grand_build(kgs_ctx_t* ctx, int kind, const uint8_t* f_mont, const uint8_t* t_mont, const uint8_t* sel_f,
+                    const uint8_t* sel_t, const uint8_t gamma_mont[32], uint64_t n, uint8_t* out_mont);
+/* Polynomial.evaluate (polynomial.js:228-238) */
+int kgs_poly_eval(kgs_ctx_t* ctx, const uint8_t* coef_mont, uint64_t len, const uint8_t x_mont[32],
+                  uint8_t out_mont[32]);
+/* Polynomial.divByXSubValue (polynomial.js:814-851); out has `len` coefficients */
+int kgs_poly_div_x_sub(kgs_ctx_t* ctx, const uint8_t* coef_mont, uint64_t len, const uint8_t z_mont[32],
+                       uint8_t* out_mont);
+/* Keccak-256 (js-sha3 keccak256) */
+int kgs_keccak256(const uint8_t* data, uint64_t len, uint8_t out[32]);
+
+/* ---- device timing helpers for bench.py (events recorded on ctx's stream) ---- */
+/* Run `reps` MSMs of n scalars (device pointer) back to back; returns total ms on the stream. */
+int kgs_bench_msm(kgs_ctx_t* ctx, const void* d_scalars_mont, uint64_t n, int reps, double* ms);
+/* Run `reps` forward+inverse NTT pairs of size 2^logm on a device buffer; returns ms. */
+int kgs_bench_ntt(kgs_ctx_t* ctx, void* d_buf, int logm, int reps, double* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KGS_H */

@@ -1,0 +1,338 @@
+"""kzg-grandsums-study_amd — MI355X-native KZG grand-sum / grand-product prover (host mirror).
+
+Python mirror of the reference's module API (xavi-pinsach/kzg-grandsums-study):
+
+    prover(pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None) -> proof
+        src/grandsum/mset_eq_kzg_prover.js:12  -> grandsum_prover
+        src/grandproduct/mset_eq_kzg_prover.js:12 -> grandproduct_prover
+
+over the C-ABI library lib/libkgs.so (include/kgs.h; HIP kernels for gfx950). The JavaScript
+drop-in modules (js/) bind the same library through an N-API addon. There is NO CPU fallback:
+if the HIP library cannot be loaded the import raises.
+
+Input/ownership conventions follow the reference exactly: F/T evaluations are
+32 B LE standard-form buffers that are overwritten with their Montgomery form (prover.js:147-148);
+selectors are Montgomery buffers; the proof is {"commitments": {name: 64 B LEM},
+"evaluations": {name: 32 B LE Montgomery}}.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libkgs.so")
+
+GRANDSUM = 0
+GRANDPRODUCT = 1
+
+R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+FR_ONE_MONT = ((1 << 256) % R).to_bytes(32, "little")
+
+_lib = None
+
+
+class KgsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+
+
+def lib():
+    """Load lib/libkgs.so (raises if it is missing: the HIP path is the only path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"HIP library not built: {LIB_PATH} (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        c_u8p = ctypes.c_void_p
+        L.kgs_last_error.restype = ctypes.c_char_p
+        L.kgs_version.restype = ctypes.c_char_p
+        L.kgs_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.kgs_ctx_destroy.argtypes = [ctypes.c_void_p]
+        L.kgs_ctx_destroy.restype = None
+        L.kgs_srs_load_ptau.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
+        L.kgs_srs_load_points.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+        L.kgs_srs_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint64),
+                                   ctypes.POINTER(ctypes.c_int)]
+        L.kgs_ptau_read_tau_g2.argtypes = [ctypes.c_char_p, c_u8p]
+        L.kgs_ptau_write_synthetic.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, c_u8p]
+        PP = ctypes.POINTER(ctypes.c_void_p)
+        L.kgs_prove.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, PP, PP, c_u8p, c_u8p,
+                                PP, PP, c_u8p, c_u8p]
+        L.kgs_prove_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, PP, PP,
+                                       ctypes.c_void_p, ctypes.c_void_p, c_u8p, c_u8p]
+        L.kgs_proof_shape.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                      ctypes.POINTER(ctypes.c_int)]
+        L.kgs_last_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+        L.kgs_fr_to_mont.argtypes = [ctypes.c_void_p, c_u8p, c_u8p, ctypes.c_uint64]
+        L.kgs_ntt.argtypes = [ctypes.c_void_p, c_u8p, c_u8p, ctypes.c_int, ctypes.c_int]
+        L.kgs_msm.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint64, c_u8p]
+        L.kgs_grand_build.argtypes = [ctypes.c_void_p, ctypes.c_int, c_u8p, c_u8p, c_u8p, c_u8p, c_u8p,
+                                      ctypes.c_uint64, c_u8p]
+        L.kgs_poly_eval.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint64, c_u8p, c_u8p]
+        L.kgs_poly_div_x_sub.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint64, c_u8p, c_u8p]
+        L.kgs_keccak256.argtypes = [c_u8p, ctypes.c_uint64, c_u8p]
+        L.kgs_bench_msm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_double)]
+        L.kgs_bench_ntt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_double)]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc < 0:
+        raise KgsError(rc, lib().kgs_last_error().decode())
+    return rc
+
+
+def _buf(b):
+    """bytes-like -> (ctypes buffer, pointer) keeping it alive."""
+    cb = ctypes.create_string_buffer(bytes(b), len(b)) if b is not None else None
+    return cb
+
+
+def keccak256(data: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    src = ctypes.create_string_buffer(bytes(data), max(1, len(data)))
+    _check(lib().kgs_keccak256(src, len(data), out))
+    return out.raw
+
+
+class Evaluations:
+    """Mirror of src/polynomial/evaluations.js (the prover's input container): `.eval` bytes."""
+
+    def __init__(self, eval_bytes):
+        self.eval = bytes(eval_bytes)
+
+    def length(self):
+        if len(self.eval) % 32:
+            raise ValueError("Polynomial evaluations buffer has incorrect size")
+        return len(self.eval) // 32
+
+    @staticmethod
+    def getOneEvals(length):
+        return Evaluations(FR_ONE_MONT * length)
+
+    def isAllOnes(self):
+        return self.eval == FR_ONE_MONT * self.length()
+
+    def isAllZeros(self):
+        return self.eval == bytes(len(self.eval))
+
+
+class Context:
+    """One HIP device + resident SRS. Not re-entrant (like the reference's curve object)."""
+
+    def __init__(self, device=0):
+        self._h = ctypes.c_void_p()
+        _check(lib().kgs_ctx_create(device, ctypes.byref(self._h)))
+        self._srs = None
+
+    def close(self):
+        if self._h:
+            lib().kgs_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def load_ptau(self, path, nbits_max=-1):
+        _check(lib().kgs_srs_load_ptau(self._h, os.fsencode(path), nbits_max))
+        self._srs = (path, nbits_max)
+
+    def srs_info(self):
+        p, c = ctypes.c_int(), ctypes.c_int()
+        n = ctypes.c_uint64()
+        _check(lib().kgs_srs_info(self._h, ctypes.byref(p), ctypes.byref(n), ctypes.byref(c)))
+        return p.value, n.value, c.value
+
+    def write_synthetic_ptau(self, path, power, tau):
+        t = ctypes.create_string_buffer(int(tau % R).to_bytes(32, "little"), 32)
+        _check(lib().kgs_ptau_write_synthetic(self._h, os.fsencode(path), power, t))
+
+    # ---- primitives (host buffers) ----
+    def fr_to_mont(self, data):
+        n = len(data) // 32
+        out = ctypes.create_string_buffer(32 * n)
+        _check(lib().kgs_fr_to_mont(self._h, _buf(data), out, n))
+        return out.raw
+
+    def ntt(self, data, inverse=False):
+        m = len(data) // 32
+        logm = m.bit_length() - 1
+        out = ctypes.create_string_buffer(32 * m)
+        _check(lib().kgs_ntt(self._h, _buf(data), out, logm, 1 if inverse else 0))
+        return out.raw
+
+    def msm(self, scalars_mont):
+        n = len(scalars_mont) // 32
+        out = ctypes.create_string_buffer(64)
+        _check(lib().kgs_msm(self._h, _buf(scalars_mont) if n else None, n, out))
+        return out.raw
+
+    def grand_build(self, kind, f_mont, t_mont, gamma_mont, sel_f=None, sel_t=None):
+        n = len(f_mont) // 32
+        out = ctypes.create_string_buffer(32 * n)
+        _check(lib().kgs_grand_build(self._h, kind, _buf(f_mont), _buf(t_mont), _buf(sel_f), _buf(sel_t),
+                                     _buf(gamma_mont), n, out))
+        return out.raw
+
+    def poly_eval(self, coef_mont, x_mont):
+        out = ctypes.create_string_buffer(32)
+        _check(lib().kgs_poly_eval(self._h, _buf(coef_mont), len(coef_mont) // 32, _buf(x_mont), out))
+        return out.raw
+
+    def poly_div_x_sub(self, coef_mont, z_mont):
+        out = ctypes.create_string_buffer(len(coef_mont))
+        _check(lib().kgs_poly_div_x_sub(self._h, _buf(coef_mont), len(coef_mont) // 32, _buf(z_mont), out))
+        return out.raw
+
+    def last_timing(self):
+        arr = (ctypes.c_double * 8)()
+        n = lib().kgs_last_timing(self._h, arr, 8)
+        return list(arr[:max(n, 0)])
+
+    # ---- full prover ----
+    def prove(self, kind, nbits, evals_f, evals_t, sel_f=None, sel_t=None, mont_out=True):
+        """Host-buffer prover; returns (commitment list, evaluation list, mont_f, mont_t)."""
+        k = len(evals_f)
+        n = 1 << nbits
+        keep = []
+        PF = (ctypes.c_void_p * k)()
+        PT = (ctypes.c_void_p * k)()
+        MF = (ctypes.c_void_p * k)()
+        MT = (ctypes.c_void_p * k)()
+        mf, mt = [], []
+        for i in range(k):
+            a, b = _buf(evals_f[i]), _buf(evals_t[i])
+            keep += [a, b]
+            PF[i] = ctypes.cast(a, ctypes.c_void_p)
+            PT[i] = ctypes.cast(b, ctypes.c_void_p)
+            ma, mb = ctypes.create_string_buffer(32 * n), ctypes.create_string_buffer(32 * n)
+            mf.append(ma)
+            mt.append(mb)
+            MF[i] = ctypes.cast(ma, ctypes.c_void_p)
+            MT[i] = ctypes.cast(mb, ctypes.c_void_p)
+        selected = sel_f is not None
+        nc, ne = ctypes.c_int(), ctypes.c_int()
+        lib().kgs_proof_shape(kind, k, 1 if selected else 0, ctypes.byref(nc), ctypes.byref(ne))
+        com = ctypes.create_string_buffer(64 * nc.value)
+        ev = ctypes.create_string_buffer(32 * ne.value)
+        sf, st = _buf(sel_f), _buf(sel_t)
+        _check(lib().kgs_prove(self._h, kind, nbits, k, PF, PT, sf, st, MF if mont_out else None,
+                               MT if mont_out else None, com, ev))
+        coms = [com.raw[64 * i:64 * i + 64] for i in range(nc.value)]
+        evs = [ev.raw[32 * i:32 * i + 32] for i in range(ne.value)]
+        return coms, evs, [m.raw for m in mf], [m.raw for m in mt]
+
+    def prove_device(self, kind, nbits, d_f, d_t, d_sf=None, d_st=None):
+        """Device-resident prover (d_* are device pointers as ints). Returns (commitments, evaluations)."""
+        k = len(d_f)
+        PF = (ctypes.c_void_p * k)(*d_f)
+        PT = (ctypes.c_void_p * k)(*d_t)
+        selected = d_sf is not None
+        nc, ne = ctypes.c_int(), ctypes.c_int()
+        lib().kgs_proof_shape(kind, k, 1 if selected else 0, ctypes.byref(nc), ctypes.byref(ne))
+        com = ctypes.create_string_buffer(64 * nc.value)
+        ev = ctypes.create_string_buffer(32 * ne.value)
+        _check(lib().kgs_prove_device(self._h, kind, nbits, k, PF, PT, d_sf, d_st, com, ev))
+        return ([com.raw[64 * i:64 * i + 64] for i in range(nc.value)],
+                [ev.raw[32 * i:32 * i + 32] for i in range(ne.value)])
+
+
+def proof_names(kind, npols, selected):
+    """Commitment / evaluation key order of the C-ABI outputs (kgs.h) in the reference's names."""
+    vec = npols > 1
+    gs = kind == GRANDSUM
+    com = []
+    for i in range(npols):
+        com += [f"F{i}" if vec else "F", f"T{i}" if vec else "T"]
+    if selected:
+        com += ["selF", "selT"]
+    com += ["S" if gs else "Z", "Q", "Wxi", "Wxiw"]
+    ev = []
+    for i in range(npols):
+        ev.append(f"f{i}xi" if vec else "fxi")
+        if gs:
+            ev.append(f"t{i}xi" if vec else "txi")
+    if selected:
+        ev += ["selFxi", "selTxi"]
+    ev.append("sxiw" if gs else "zxiw")
+    return com, ev
+
+
+_CTX = {}
+
+
+def _context(device=0):
+    if device not in _CTX:
+        _CTX[device] = Context(device)
+    return _CTX[device]
+
+
+def _prover(kind, pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, device=0):
+    """src/grandsum/mset_eq_kzg_prover.js:12-142 — input checks with the reference's messages, then
+    the HIP prover. Overwrites evalsFs[i].eval / evalsTs[i].eval with Montgomery form (:147-148)."""
+    if not isinstance(evalsFs, (list, tuple)):
+        evalsFs = [evalsFs]
+    if not isinstance(evalsTs, (list, tuple)):
+        evalsTs = [evalsTs]
+    if len(evalsFs) != len(evalsTs):
+        raise ValueError("The lengths of the two vector multisets must be the same.")
+    npols = len(evalsFs)
+    if npols == 0:
+        raise ValueError("The number of multisets must be greater than 0.")
+    for i in range(npols):
+        if evalsFs[i].length() != evalsTs[i].length():
+            raise ValueError(f"The {i}-th multiset buffers must have the same length.")
+        elif evalsFs[i].length() != evalsFs[0].length():
+            raise ValueError("The multiset buffers must all have the same length.")
+    n0 = evalsFs[0].length()
+    if evalsSelF is None:
+        evalsSelF = Evaluations.getOneEvals(n0)
+    if evalsSelT is None:
+        evalsSelT = Evaluations.getOneEvals(n0)
+    if evalsSelF.length() != evalsSelT.length():
+        raise ValueError("The selection buffers must have the same length.")
+    elif evalsSelF.length() != n0:
+        raise ValueError("The selection buffers must have the same length as the multiset buffers.")
+    is_selected = not (evalsSelF.isAllOnes() and evalsSelT.isAllOnes())
+    nbits = (n0 - 1).bit_length() if n0 > 0 else 0
+    if n0 != (1 << nbits):
+        raise ValueError("Polynomial length must be a power of two.")
+    ctx = _context(device)
+    ctx.load_ptau(pTauFilename)
+    power, _, _ = ctx.srs_info()
+    if power < nbits:
+        raise ValueError("The Powers of Tau file is not sufficiently large to commit the polynomials.")
+    coms, evs, mf, mt = ctx.prove(kind, nbits, [e.eval for e in evalsFs], [e.eval for e in evalsTs],
+                                  evalsSelF.eval if is_selected else None,
+                                  evalsSelT.eval if is_selected else None)
+    for i in range(npols):
+        evalsFs[i].eval = mf[i]
+        evalsTs[i].eval = mt[i]
+    cn, en = proof_names(kind, npols, is_selected)
+    return {"commitments": dict(zip(cn, coms)), "evaluations": dict(zip(en, evs))}
+
+
+def grandsum_prover(pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, device=0):
+    """mset_eq_kzg_grandsum_prover (src/grandsum/mset_eq_kzg_prover.js:12)."""
+    try:
+        return _prover(GRANDSUM, pTauFilename, evalsFs, evalsTs, evalsSelF, evalsSelT, device)
+    except KgsError as e:
+        raise ValueError(str(e)) from e
+
+
+def grandproduct_prover(pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, device=0):
+    """mset_eq_kzg_grandproduct_prover (src/grandproduct/mset_eq_kzg_prover.js:12)."""
+    try:
+        return _prover(GRANDPRODUCT, pTauFilename, evalsFs, evalsTs, evalsSelF, evalsSelT, device)
+    except KgsError as e:
+        raise ValueError(str(e)) from e

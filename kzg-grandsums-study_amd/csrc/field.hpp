@@ -1,0 +1,325 @@
+// BN254 Fr / Fq Montgomery arithmetic for gfx950 (device) — 8 x 32-bit little-endian limbs.
+//
+// Representation: identical bytes to ffjavascript's in-memory form (32 B LE, Montgomery with
+// R = 2^256), so ptau LEM points and caller buffers are used without conversion. Both moduli are
+// < 2^254, which enables the "no-carry" CIOS variant (no t[N], t[N+1] words).
+//
+// Replaces the [ffjs] wasm field (`curve.Fr.*`, `curve.F1.*`) on the hot path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kgs {
+
+struct FqP {
+  static constexpr uint32_t p[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
+                                    0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t inv = 0xe4866389u;  // -p^-1 mod 2^32
+  static constexpr uint32_t one[8] = {0xc58f0d9du, 0xd35d438du, 0xf5c70b3du, 0x0a78eb28u,
+                                      0x7879462cu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr uint32_t r2[8] = {0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u,
+                                     0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u};
+};
+
+struct FrP {
+  static constexpr uint32_t p[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                                    0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t inv = 0xefffffffu;
+  static constexpr uint32_t one[8] = {0x4ffffffbu, 0xac96341cu, 0x9f60cd29u, 0x36fc7695u,
+                                      0x7879462eu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr uint32_t r2[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
+                                     0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
+};
+
+template <class P>
+struct Fe {
+  uint32_t v[8];
+
+  __device__ __forceinline__ static Fe zero() {
+    Fe r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = 0;
+    return r;
+  }
+  __device__ __forceinline__ static Fe one() {
+    Fe r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = P::one[i];
+    return r;
+  }
+  __device__ __forceinline__ bool is_zero() const {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc |= v[i];
+    return acc == 0;
+  }
+  __device__ __forceinline__ bool operator==(const Fe& o) const {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc |= v[i] ^ o.v[i];
+    return acc == 0;
+  }
+  __device__ __forceinline__ bool operator!=(const Fe& o) const { return !(*this == o); }
+
+  // r = a - p if a >= p (a < 2p)
+  __device__ __forceinline__ static Fe reduce_once(const Fe& a) {
+    Fe d;
+    uint32_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      uint64_t s = (uint64_t)a.v[i] - P::p[i] - borrow;
+      d.v[i] = (uint32_t)s;
+      borrow = (uint32_t)(s >> 63);
+    }
+    Fe r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = borrow ? a.v[i] : d.v[i];
+    return r;
+  }
+
+  __device__ __forceinline__ friend Fe operator+(const Fe& a, const Fe& b) {
+    Fe s;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      uint64_t t = (uint64_t)a.v[i] + b.v[i] + c;
+      s.v[i] = (uint32_t)t;
+      c = (uint32_t)(t >> 32);
+    }
+    return reduce_once(s);
+  }
+
+  __device__ __forceinline__ friend Fe operator-(const Fe& a, const Fe& b) {
+    Fe d;
+    uint32_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      uint64_t t = (uint64_t)a.v[i] - b.v[i] - borrow;
+      d.v[i] = (uint32_t)t;
+      borrow = (uint32_t)(t >> 63);
+    }
+    // if borrow: d += p
+    uint32_t mask = 0u - borrow, c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      uint64_t t = (uint64_t)d.v[i] + (P::p[i] & mask) + c;
+      d.v[i] = (uint32_t)t;
+      c = (uint32_t)(t >> 32);
+    }
+    return d;
+  }
+
+  __device__ __forceinline__ Fe neg() const { return is_zero() ? *this : (zero() - *this); }
+  __device__ __forceinline__ Fe dbl() const { return *this + *this; }
+
+  // Montgomery product (CIOS, no-carry variant: valid because p[7] < 2^31 - 1).
+  __device__ __forceinline__ friend Fe operator*(const Fe& a, const Fe& b) {
+    uint32_t t[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) t[j] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      uint64_t p = (uint64_t)a.v[0] * b.v[i] + t[0];
+      uint32_t A = (uint32_t)(p >> 32);
+      t[0] = (uint32_t)p;
+      uint32_t m = t[0] * P::inv;
+      uint64_t q = (uint64_t)m * P::p[0] + t[0];
+      uint32_t C = (uint32_t)(q >> 32);
+#pragma unroll
+      for (int j = 1; j < 8; j++) {
+        p = (uint64_t)a.v[j] * b.v[i] + t[j] + A;
+        A = (uint32_t)(p >> 32);
+        t[j] = (uint32_t)p;
+        q = (uint64_t)m * P::p[j] + t[j] + C;
+        C = (uint32_t)(q >> 32);
+        t[j - 1] = (uint32_t)q;
+      }
+      t[7] = C + A;
+    }
+    Fe r;
+#pragma unroll
+    for (int j = 0; j < 8; j++) r.v[j] = t[j];
+    return reduce_once(r);
+  }
+
+  __device__ __forceinline__ Fe sqr() const { return (*this) * (*this); }
+
+  __device__ __forceinline__ Fe to_mont() const {
+    Fe r2;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r2.v[i] = P::r2[i];
+    return (*this) * r2;
+  }
+  __device__ __forceinline__ Fe from_mont() const {
+    Fe o = zero();
+    o.v[0] = 1;
+    return (*this) * o;
+  }
+
+  // a^(p-2) (Fermat); 0 -> 0. Latency-heavy: use only off the critical path / once per tile.
+  __device__ Fe inverse() const {
+    // exponent e = p - 2, scanned from the top bit, 4-bit fixed windows
+    Fe tbl[16];
+    tbl[0] = one();
+    tbl[1] = *this;
+#pragma unroll
+    for (int i = 2; i < 16; i++) tbl[i] = tbl[i - 1] * (*this);
+    Fe r = one();
+    for (int w = 63; w >= 0; w--) {
+      const int limb = w >> 3, sh = (w & 7) * 4;
+      uint32_t e = P::p[limb];
+      if (limb == 0) e -= 2;  // p - 2 (no borrow: p[0] >= 2 for both moduli)
+      uint32_t d = (e >> sh) & 15u;
+      r = r.sqr();
+      r = r.sqr();
+      r = r.sqr();
+      r = r.sqr();
+      if (d) {
+        Fe m = tbl[0];
+        for (int k = 1; k < 16; k++)
+          if ((uint32_t)k == d) m = tbl[k];
+        r = r * m;
+      }
+    }
+    return r;
+  }
+
+  __device__ __forceinline__ static Fe load(const uint32_t* p) {
+    Fe r;
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint4 a = q[0], b = q[1];
+    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+    return r;
+  }
+  __device__ __forceinline__ void store(uint32_t* p) const {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    q[0] = make_uint4(v[0], v[1], v[2], v[3]);
+    q[1] = make_uint4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+using fr = Fe<FrP>;
+using fq = Fe<FqP>;
+
+// ------------------------------------------------------------------------------------- G1
+// Affine storage: 64 B (x||y, Montgomery Fq) == ptau LEM; infinity == (0,0).
+struct g1_aff {
+  fq x, y;
+  __device__ __forceinline__ bool is_inf() const { return x.is_zero() && y.is_zero(); }
+  __device__ __forceinline__ static g1_aff load(const uint32_t* p) {
+    g1_aff a;
+    a.x = fq::load(p);
+    a.y = fq::load(p + 8);
+    return a;
+  }
+};
+
+// XYZZ coordinates: x = X/ZZ, y = Y/ZZZ; infinity <=> ZZ == 0.
+struct g1_xyzz {
+  fq X, Y, ZZ, ZZZ;
+
+  __device__ __forceinline__ static g1_xyzz inf() {
+    g1_xyzz r;
+    r.X = fq::one(); r.Y = fq::one(); r.ZZ = fq::zero(); r.ZZZ = fq::zero();
+    return r;
+  }
+  __device__ __forceinline__ bool is_inf() const { return ZZ.is_zero(); }
+  __device__ __forceinline__ static g1_xyzz from_aff(const g1_aff& a) {
+    if (a.is_inf()) return inf();
+    g1_xyzz r;
+    r.X = a.x; r.Y = a.y; r.ZZ = fq::one(); r.ZZZ = fq::one();
+    return r;
+  }
+  __device__ __forceinline__ static g1_xyzz load(const uint32_t* p) {
+    g1_xyzz r;
+    r.X = fq::load(p); r.Y = fq::load(p + 8); r.ZZ = fq::load(p + 16); r.ZZZ = fq::load(p + 24);
+    return r;
+  }
+  __device__ __forceinline__ void store(uint32_t* p) const {
+    X.store(p); Y.store(p + 8); ZZ.store(p + 16); ZZZ.store(p + 24);
+  }
+
+  // dbl-2008-s-1 (a = 0)
+  __device__ g1_xyzz dbl() const {
+    if (is_inf()) return *this;
+    fq U = Y.dbl();
+    fq V = U.sqr();
+    fq W = U * V;
+    fq S = X * V;
+    fq X2 = X.sqr();
+    fq M = X2.dbl() + X2;
+    g1_xyzz r;
+    r.X = M.sqr() - S.dbl();
+    r.Y = M * (S - r.X) - W * Y;
+    r.ZZ = V * ZZ;
+    r.ZZZ = W * ZZZ;
+    return r;
+  }
+
+  // mdbl-2008-s-1: 2*affine
+  __device__ static g1_xyzz dbl_aff(const g1_aff& a) {
+    fq U = a.y.dbl();
+    fq V = U.sqr();
+    fq W = U * V;
+    fq S = a.x * V;
+    fq X2 = a.x.sqr();
+    fq M = X2.dbl() + X2;
+    g1_xyzz r;
+    r.X = M.sqr() - S.dbl();
+    r.Y = M * (S - r.X) - W * a.y;
+    r.ZZ = V;
+    r.ZZZ = W;
+    return r;
+  }
+
+  // madd-2008-s: this += affine (handles infinity / equal / opposite)
+  __device__ void add_aff(const g1_aff& a) {
+    if (a.is_inf()) return;
+    if (is_inf()) { *this = from_aff(a); return; }
+    fq U2 = a.x * ZZ;
+    fq S2 = a.y * ZZZ;
+    fq P = U2 - X;
+    fq R = S2 - Y;
+    if (P.is_zero()) {
+      if (R.is_zero()) { *this = dbl_aff(a); return; }
+      *this = inf();
+      return;
+    }
+    fq PP = P.sqr();
+    fq PPP = P * PP;
+    fq Qv = X * PP;
+    fq nX = R.sqr() - PPP - Qv.dbl();
+    Y = R * (Qv - nX) - Y * PPP;
+    X = nX;
+    ZZ = ZZ * PP;
+    ZZZ = ZZZ * PPP;
+  }
+
+  // add-2008-s: this += other
+  __device__ void add(const g1_xyzz& o) {
+    if (o.is_inf()) return;
+    if (is_inf()) { *this = o; return; }
+    fq U1 = X * o.ZZ;
+    fq U2 = o.X * ZZ;
+    fq S1 = Y * o.ZZZ;
+    fq S2 = o.Y * ZZZ;
+    fq P = U2 - U1;
+    fq R = S2 - S1;
+    if (P.is_zero()) {
+      if (R.is_zero()) { *this = dbl(); return; }
+      *this = inf();
+      return;
+    }
+    fq PP = P.sqr();
+    fq PPP = P * PP;
+    fq Qv = U1 * PP;
+    fq nX = R.sqr() - PPP - Qv.dbl();
+    Y = R * (Qv - nX) - S1 * PPP;
+    X = nX;
+    ZZ = ZZ * o.ZZ * PP;
+    ZZZ = ZZZ * o.ZZZ * PPP;
+  }
+};
+
+}  // namespace kgs

@@ -1,0 +1,75 @@
+// Launch wrappers for the gfx950 kernels (ntt.hip, poly.hip, msm.hip). All pointers are device
+// pointers to 32 B Montgomery Fr elements (uint32_t[8]) or 64 B affine / 128 B XYZZ G1 points,
+// unless stated otherwise. Launches are asynchronous on `st`.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "field.hpp"
+
+namespace kgs {
+
+constexpr int LC_MAX = 32;
+struct LinComb {  // out[i] = sum_k coef_k * src_k[i] (zero beyond len_k) + (i == 0 ? c0 : 0)
+  int nterms;
+  const uint32_t* src[LC_MAX];
+  uint64_t len[LC_MAX];
+  uint32_t coef[LC_MAX][8];
+  uint32_t c0[8];
+};
+
+constexpr int EB_MAX = 32;
+struct EvalBatch {
+  int npolys;
+  const uint32_t* src[EB_MAX];
+  uint64_t len[EB_MAX];
+};
+
+struct MsmTables {
+  uint32_t* table = nullptr;  // W x npts affine points (64 B)
+  uint64_t npts = 0;
+  int c = 0, W = 0;
+};
+
+struct MsmWork {
+  int32_t* digit = nullptr;
+  uint32_t *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *sorted = nullptr;
+  uint32_t *bstart = nullptr, *segpart = nullptr, *buckets = nullptr, *part = nullptr;
+};
+
+// ntt.hip
+void ntt_dif(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t in_len, int logm, const uint32_t* pre,
+             const uint32_t* tw, int logM);
+void ntt_dit(hipStream_t st, uint32_t* out, const uint32_t* in, int in_bitrev, int logm, const uint32_t* tw, int logM,
+             const uint32_t* post, const uint32_t* post_s);
+void launch_powers(hipStream_t st, uint32_t* out, uint64_t count, const uint32_t* w_dev, const uint32_t* scale_dev);
+void launch_scale_copy(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t n, const uint32_t* tab,
+                       const uint32_t* sc);
+void launch_bitrev_copy(hipStream_t st, uint32_t* out, const uint32_t* in, int logm);
+
+// poly.hip
+void launch_to_mont(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t n);
+void launch_lincomb(hipStream_t st, uint32_t* out, uint64_t n, const LinComb& lc);
+void launch_builder(hipStream_t st, bool prod, bool sel, uint32_t* out, const uint32_t* f, const uint32_t* t,
+                    const uint32_t* sf, const uint32_t* stt, const uint32_t* gamma, uint64_t n, uint32_t* scratch_tp,
+                    uint32_t* scratch_ti, uint32_t* flag);
+void launch_quotient(hipStream_t st, bool prod, bool sel, uint32_t* q, const uint32_t* S, const uint32_t* F,
+                     const uint32_t* T, const uint32_t* SF, const uint32_t* ST, const uint32_t* inv_nxm1,
+                     const uint32_t* scalars, int lcs, uint32_t rot);
+void launch_divcheck(hipStream_t st, bool prod, bool sel, uint32_t* flag, const uint32_t* S, const uint32_t* f,
+                     const uint32_t* t, const uint32_t* sf, const uint32_t* stt, const uint32_t* scalars, uint64_t n);
+void launch_eval_tiles(hipStream_t st, uint32_t* part, const EvalBatch& eb, const uint32_t* xp, uint32_t ntiles_max);
+void launch_divide(hipStream_t st, uint32_t* q, uint32_t* flag, const uint32_t* a, uint64_t L, const uint32_t* xp,
+                   uint32_t* part, uint32_t* carry);
+void launch_fr_batch_inv(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t n);
+void launch_nxm1(hipStream_t st, uint32_t* out, const uint32_t* tw, uint64_t halfM, const uint32_t* gp,
+                 const uint32_t* np, int lcs, uint64_t wstride);
+constexpr uint64_t EVAL_TILE = 2048;
+
+// msm.hip
+void msm_build_table(hipStream_t st, uint32_t* table, uint64_t npts, int c, int W, uint32_t* tmp_xyzz,
+                     uint32_t* scratch);
+void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* scalars, uint64_t N, uint32_t* T_out);
+void launch_fixed_base(hipStream_t st, uint32_t* out_xyzz, const uint32_t* sc, uint64_t count, const uint32_t* tbl);
+void launch_batch_affine(hipStream_t st, uint32_t* out_aff, const uint32_t* in_xyzz, uint32_t* scratch, uint64_t npts);
+
+}  // namespace kgs

@@ -1,0 +1,293 @@
+// BN254-G1 multi-scalar multiplication for gfx950 — replaces [ffjs] `G1.multiExpAffine` +
+// `G1.toAffine` + `Fr.batchFromMontgomery` (polynomial.js:1106-1115).
+//
+// Design (MI355X-first):
+//  * The SRS is fixed across proofs, so each base P_i is expanded ONCE into W = ceil(255/c)
+//    window copies 2^(c*j)·P_i (affine, 64 B, table[j][i]; 1.7-2 GB at n = 2^20 — HBM is 288 GB).
+//    A commitment then needs a single set of B = 2^(c-1) signed-digit buckets shared by all
+//    windows: no per-window bucket reduction and no serial 2^c-doubling window combine.
+//  * scalars leave Montgomery form and are recoded into W signed c-bit digits (digit kernel);
+//  * counting sort of the N*W (digit -> point) entries by bucket (histogram, scan, scatter);
+//  * bucket accumulation over FIXED-SIZE segments of the sorted array (load balanced whatever
+//    the bucket sizes): one XYZZ mixed-add chain per segment, runs that straddle a segment
+//    boundary are written as partials and merged by a per-bucket combine kernel;
+//  * sum_b b·S_b = sum_k 2^k T_k with T_k = sum_{b has bit k} S_b: c independent tree
+//    reductions (chip-parallel), then the c-term Horner + affine conversion on the host.
+#include "kernels.hpp"
+
+namespace kgs {
+
+static inline unsigned nb(uint64_t work, unsigned bs = 256) { return (unsigned)((work + bs - 1) / bs); }
+
+// ------------------------------------------------------------------ window table precompute
+__global__ void __launch_bounds__(256) k_tab_dbl(uint32_t* __restrict__ tmp, const uint32_t* __restrict__ prev,
+                                                 uint64_t npts, int c) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npts) return;
+  g1_aff a = g1_aff::load(prev + 16 * i);
+  g1_xyzz r = g1_xyzz::from_aff(a);
+  for (int k = 0; k < c; k++) r = r.dbl();
+  r.store(tmp + 32 * i);
+}
+
+// XYZZ -> affine with a per-thread Montgomery batch inversion over CH consecutive points.
+template <int CH>
+__global__ void __launch_bounds__(256) k_batch_affine(uint32_t* __restrict__ out, const uint32_t* __restrict__ in,
+                                                      uint32_t* __restrict__ scratch, uint64_t npts) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t start = t * CH;
+  if (start >= npts) return;
+  const uint64_t end = start + CH < npts ? start + CH : npts;
+  fq acc = fq::one();
+  for (uint64_t i = start; i < end; i++) {
+    acc.store(scratch + 8 * i);  // prefix product before i
+    fq zz = fq::load(in + 32 * i + 16), zzz = fq::load(in + 32 * i + 24);
+    if (!zz.is_zero()) acc = acc * (zz * zzz);
+  }
+  fq inv = acc.inverse();
+  for (uint64_t i = end; i-- > start;) {
+    fq zz = fq::load(in + 32 * i + 16), zzz = fq::load(in + 32 * i + 24);
+    if (zz.is_zero()) {
+      fq::zero().store(out + 16 * i);
+      fq::zero().store(out + 16 * i + 8);
+      continue;
+    }
+    fq pre = fq::load(scratch + 8 * i);
+    fq zinv = inv * pre;  // 1/(ZZ*ZZZ)
+    inv = inv * (zz * zzz);
+    fq x = fq::load(in + 32 * i) * (zinv * zzz);
+    fq y = fq::load(in + 32 * i + 8) * (zinv * zz);
+    x.store(out + 16 * i);
+    y.store(out + 16 * i + 8);
+  }
+}
+
+void msm_build_table(hipStream_t st, uint32_t* table, uint64_t npts, int c, int W, uint32_t* tmp_xyzz,
+                     uint32_t* scratch) {
+  for (int j = 1; j < W; j++) {
+    const uint32_t* prev = table + (uint64_t)(j - 1) * npts * 16;
+    uint32_t* cur = table + (uint64_t)j * npts * 16;
+    hipLaunchKernelGGL(k_tab_dbl, dim3(nb(npts)), dim3(256), 0, st, tmp_xyzz, prev, npts, c);
+    hipLaunchKernelGGL(k_batch_affine<32>, dim3(nb((npts + 31) / 32)), dim3(256), 0, st, cur, tmp_xyzz,
+                       scratch, npts);
+  }
+}
+
+// ------------------------------------------------------------------ digits + counting sort
+// digit[j*N + i] = signed c-bit digit j of from_mont(scalar_i); |digit| in [0, 2^(c-1)]
+__global__ void __launch_bounds__(256) k_digits(int32_t* __restrict__ digit, const uint32_t* __restrict__ sc,
+                                                uint64_t N, int c, int W) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  fr s = fr::load(sc + 8 * i).from_mont();
+  const int32_t half = 1 << (c - 1);
+  const uint32_t mask = (1u << c) - 1;
+  uint32_t carry = 0;
+  for (int j = 0; j < W; j++) {
+    const int bit = j * c;
+    const int limb = bit >> 5, off = bit & 31;
+    uint64_t w = limb < 8 ? s.v[limb] : 0;
+    if (limb + 1 < 8) w |= (uint64_t)s.v[limb + 1] << 32;
+    int32_t d = (int32_t)((w >> off) & mask) + (int32_t)carry;
+    if (d > half) {
+      d -= (1 << c);
+      carry = 1;
+    } else {
+      carry = 0;
+    }
+    digit[(uint64_t)j * N + i] = d;
+  }
+}
+
+__global__ void k_hist(uint32_t* __restrict__ counts, const int32_t* __restrict__ digit, uint64_t E) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  int32_t d = digit[e];
+  if (d) atomicAdd(&counts[d < 0 ? -d : d], 1u);
+}
+
+// exclusive scan of counts[0..nb) into offsets[0..nb] (single block of 1024 threads)
+__global__ void __launch_bounds__(1024) k_scan_u32(uint32_t* __restrict__ offsets, uint32_t* __restrict__ cursor,
+                                                   const uint32_t* __restrict__ counts, uint32_t nbins) {
+  __shared__ uint32_t part[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (nbins + 1023) / 1024;
+  uint32_t lo = t * per, hi = lo + per < nbins ? lo + per : nbins;
+  uint32_t s = 0;
+  for (uint32_t i = lo; i < hi; i++) s += counts[i];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    uint32_t v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = t ? part[t - 1] : 0;
+  for (uint32_t i = lo; i < hi; i++) {
+    offsets[i] = run;
+    cursor[i] = run;
+    run += counts[i];
+  }
+  if (t == 1023) offsets[nbins] = part[1023];
+}
+
+// sorted[pos] = (j*Nsrs + i) | sign<<31
+__global__ void k_scatter(uint32_t* __restrict__ sorted, uint32_t* __restrict__ cursor,
+                          const int32_t* __restrict__ digit, uint64_t E, uint64_t N, uint64_t Nsrs) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  int32_t d = digit[e];
+  if (!d) return;
+  uint32_t k = d < 0 ? -d : d;
+  uint32_t pos = atomicAdd(&cursor[k], 1u);
+  uint64_t j = e / N, i = e - j * N;
+  sorted[pos] = (uint32_t)(j * Nsrs + i) | (d < 0 ? 0x80000000u : 0u);
+}
+
+// ------------------------------------------------------------------ bucket accumulation
+__device__ __forceinline__ void emit_run(uint32_t* bstart, uint32_t* segpart, uint32_t b, uint64_t rs,
+                                         const uint32_t* offsets, uint64_t seg, const g1_xyzz& acc) {
+  if (rs == offsets[b])
+    acc.store(bstart + 32 * (uint64_t)b);
+  else
+    acc.store(segpart + 32 * seg);
+}
+
+__global__ void __launch_bounds__(256) k_accumulate(uint32_t* __restrict__ bstart, uint32_t* __restrict__ segpart,
+                                                    const uint32_t* __restrict__ sorted,
+                                                    const uint32_t* __restrict__ offsets, uint32_t nbins,
+                                                    const uint32_t* __restrict__ table, uint32_t L) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t E = offsets[nbins];
+  const uint64_t start = s * L;
+  if (start >= E) return;
+  const uint64_t end = start + L < E ? start + L : E;
+  // largest b with offsets[b] <= start (offsets nondecreasing, offsets[0] == 0)
+  uint32_t lo = 0, hi = nbins;  // invariant offsets[lo] <= start < offsets[hi]
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (offsets[mid] <= start) lo = mid; else hi = mid;
+  }
+  uint32_t b = lo;
+  uint64_t rs = start;
+  uint64_t bend = offsets[b + 1];
+  g1_xyzz acc = g1_xyzz::inf();
+  for (uint64_t e = start; e < end; e++) {
+    if (e >= bend) {
+      emit_run(bstart, segpart, b, rs, offsets, s, acc);
+      do { b++; bend = offsets[b + 1]; } while (e >= bend);
+      rs = e;
+      acc = g1_xyzz::inf();
+    }
+    uint32_t v = sorted[e];
+    g1_aff p = g1_aff::load(table + 16 * (uint64_t)(v & 0x7fffffffu));
+    if (v & 0x80000000u) p.y = p.y.neg();
+    acc.add_aff(p);
+  }
+  emit_run(bstart, segpart, b, rs, offsets, s, acc);
+}
+
+__global__ void __launch_bounds__(256) k_combine(uint32_t* __restrict__ buckets, const uint32_t* __restrict__ bstart,
+                                                 const uint32_t* __restrict__ segpart,
+                                                 const uint32_t* __restrict__ offsets, uint32_t B, uint32_t L) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x + 1;  // buckets 1..B
+  if (b > B) return;
+  const uint64_t o0 = offsets[b], o1 = offsets[b + 1];
+  g1_xyzz acc = g1_xyzz::inf();
+  if (o1 > o0) {
+    acc = g1_xyzz::load(bstart + 32 * (uint64_t)b);
+    for (uint64_t sgm = o0 / L + 1; sgm * L < o1; sgm++) acc.add(g1_xyzz::load(segpart + 32 * sgm));
+  }
+  acc.store(buckets + 32 * (uint64_t)b);
+}
+
+// ------------------------------------------------------------------ sum_b b*S_b via bit sums
+// block (k, chunk): tree-sum of the buckets b in [1, B-1] with bit k set (k < c-1), t-th such
+// bucket: insert a 1 at bit k of t. k == c-1: bucket B alone.
+__global__ void __launch_bounds__(256) k_bitsum1(uint32_t* __restrict__ part, const uint32_t* __restrict__ buckets,
+                                                 int c, uint32_t chunks) {
+  __shared__ uint32_t lds[256 * 32];
+  const int k = blockIdx.y;
+  const uint32_t chunk = blockIdx.x;
+  const uint32_t B = 1u << (c - 1);
+  const uint32_t t = chunk * 256 + threadIdx.x;
+  g1_xyzz v = g1_xyzz::inf();
+  if (k == c - 1) {
+    if (t == 0) v = g1_xyzz::load(buckets + 32 * (uint64_t)B);
+  } else if (t < B / 2) {
+    uint32_t b = ((t >> k) << (k + 1)) | (1u << k) | (t & ((1u << k) - 1));
+    v = g1_xyzz::load(buckets + 32 * (uint64_t)b);
+  }
+  for (int stride = 128; stride > 0; stride >>= 1) {
+    if (threadIdx.x >= stride && threadIdx.x < 2 * stride) v.store(lds + 32 * (threadIdx.x - stride));
+    __syncthreads();
+    if (threadIdx.x < stride) v.add(g1_xyzz::load(lds + 32 * threadIdx.x));
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) v.store(part + 32 * ((uint64_t)k * chunks + chunk));
+}
+
+__global__ void __launch_bounds__(256) k_bitsum2(uint32_t* __restrict__ T, const uint32_t* __restrict__ part,
+                                                 uint32_t chunks) {
+  __shared__ uint32_t lds[256 * 32];
+  const int k = blockIdx.x;
+  g1_xyzz v = g1_xyzz::inf();
+  for (uint32_t i = threadIdx.x; i < chunks; i += 256) v.add(g1_xyzz::load(part + 32 * ((uint64_t)k * chunks + i)));
+  for (int stride = 128; stride > 0; stride >>= 1) {
+    if (threadIdx.x >= stride && threadIdx.x < 2 * stride) v.store(lds + 32 * (threadIdx.x - stride));
+    __syncthreads();
+    if (threadIdx.x < stride) v.add(g1_xyzz::load(lds + 32 * threadIdx.x));
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) v.store(T + 32 * (uint64_t)k);
+}
+
+// ------------------------------------------------------------------ driver (device part)
+void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* scalars, uint64_t N,
+             uint32_t* T_out) {
+  const int c = tb.c, W = tb.W;
+  const uint32_t B = 1u << (c - 1);
+  const uint64_t E = N * (uint64_t)W;
+  hipMemsetAsync(w.counts, 0, sizeof(uint32_t) * (B + 2), st);
+  hipLaunchKernelGGL(k_digits, dim3(nb(N)), dim3(256), 0, st, w.digit, scalars, N, c, W);
+  hipLaunchKernelGGL(k_hist, dim3(nb(E)), dim3(256), 0, st, w.counts, w.digit, E);
+  hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, st, w.offsets, w.cursor, w.counts, B + 1);
+  hipLaunchKernelGGL(k_scatter, dim3(nb(E)), dim3(256), 0, st, w.sorted, w.cursor, w.digit, E, N, tb.npts);
+  uint64_t L = E >> 18;
+  if (L < 4) L = 4;
+  if (L > 64) L = 64;
+  const uint64_t nseg = (E + L - 1) / L;
+  hipLaunchKernelGGL(k_accumulate, dim3(nb(nseg)), dim3(256), 0, st, w.bstart, w.segpart, w.sorted, w.offsets,
+                     B + 1, tb.table, (uint32_t)L);
+  hipLaunchKernelGGL(k_combine, dim3(nb(B)), dim3(256), 0, st, w.buckets, w.bstart, w.segpart, w.offsets, B,
+                     (uint32_t)L);
+  const uint32_t chunks = (B / 2 + 255) / 256 > 0 ? (B / 2 + 255) / 256 : 1;
+  hipLaunchKernelGGL(k_bitsum1, dim3(chunks, c), dim3(256), 0, st, w.part, w.buckets, c, chunks);
+  hipLaunchKernelGGL(k_bitsum2, dim3(c), dim3(256), 0, st, T_out, w.part, chunks);
+}
+
+// ------------------------------------------------------------------ fixed-base (synthetic SRS)
+// out[i] = s_i * G with s_i = from_mont(sc[i]); tbl[j*256 + d] = (d * 2^(8j)) G, affine.
+__global__ void __launch_bounds__(256) k_fixed_base(uint32_t* __restrict__ out_xyzz, const uint32_t* __restrict__ sc,
+                                                    uint64_t count, const uint32_t* __restrict__ tbl) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  fr s = fr::load(sc + 8 * i).from_mont();
+  g1_xyzz acc = g1_xyzz::inf();
+  for (int j = 0; j < 32; j++) {
+    uint32_t d = (s.v[j >> 2] >> ((j & 3) * 8)) & 0xffu;
+    if (d) acc.add_aff(g1_aff::load(tbl + 16 * ((uint64_t)j * 256 + d)));
+  }
+  acc.store(out_xyzz + 32 * i);
+}
+
+void launch_fixed_base(hipStream_t st, uint32_t* out_xyzz, const uint32_t* sc, uint64_t count, const uint32_t* tbl) {
+  hipLaunchKernelGGL(k_fixed_base, dim3(nb(count)), dim3(256), 0, st, out_xyzz, sc, count, tbl);
+}
+
+void launch_batch_affine(hipStream_t st, uint32_t* out_aff, const uint32_t* in_xyzz, uint32_t* scratch, uint64_t npts) {
+  hipLaunchKernelGGL(k_batch_affine<32>, dim3(nb((npts + 31) / 32)), dim3(256), 0, st, out_aff, in_xyzz, scratch, npts);
+}
+
+}  // namespace kgs

@@ -1,0 +1,627 @@
+// Per-element / scan / reduction kernels of the prover hot path (gfx950):
+//   * Montgomery conversion ([ffjs] Fr.batchToMontgomery, prover.js:147-148)            — A1
+//   * linear combinations (Polynomial.add/sub/mulScalar/addScalar, polynomial.js:276-422) — A9
+//   * grand-sum / grand-product builder: num/den, tile Montgomery batch inverse, prefix
+//     sum / product with tile carries (grandsum.js:6-62, grandproduct.js:6-57)          — A6-A8
+//   * quotient on a coset + divisibility check on H (replaces the 2n/4n `multiply` chain +
+//     `divZh`, prover.js:233-286, polynomial.js:352-376,853-888)                         — A4,A10
+//   * tiled Horner evaluation (polynomial.js:228-238)                                    — A11
+//   * synthetic division by (X - z) as a linear-recurrence scan (polynomial.js:814-851)  — A12
+// Every kernel is integer arithmetic on 32 B Montgomery elements; most are VALU bound (one or
+// more 254-bit Montgomery products per element), the rest HBM bound.
+#include "kernels.hpp"
+
+namespace kgs {
+
+static inline unsigned nb(uint64_t work, unsigned bs = 256) { return (unsigned)((work + bs - 1) / bs); }
+
+__device__ __forceinline__ uint32_t brev(uint32_t x, int bits) {
+  return bits ? __builtin_bitreverse32(x) >> (32 - bits) : 0;
+}
+
+// ---------------------------------------------------------------------------- conversions
+__global__ void k_to_mont(uint32_t* __restrict__ out, const uint32_t* __restrict__ in, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fr::load(in + 8 * i).to_mont().store(out + 8 * i);
+}
+void launch_to_mont(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t n) {
+  hipLaunchKernelGGL(k_to_mont, dim3(nb(n)), dim3(256), 0, st, out, in, n);
+}
+
+// ---------------------------------------------------------------------------- linear combination
+__global__ void k_lincomb(uint32_t* __restrict__ out, uint64_t n, LinComb lc) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fr acc = fr::zero();
+  for (int k = 0; k < lc.nterms; k++) {
+    if (i < lc.len[k]) {
+      fr x = fr::load(lc.src[k] + 8 * i);
+      fr c;
+#pragma unroll
+      for (int j = 0; j < 8; j++) c.v[j] = lc.coef[k][j];
+      acc = acc + x * c;
+    }
+  }
+  if (i == 0) {
+    fr c;
+#pragma unroll
+    for (int j = 0; j < 8; j++) c.v[j] = lc.c0[j];
+    acc = acc + c;
+  }
+  acc.store(out + 8 * i);
+}
+void launch_lincomb(hipStream_t st, uint32_t* out, uint64_t n, const LinComb& lc) {
+  hipLaunchKernelGGL(k_lincomb, dim3(nb(n)), dim3(256), 0, st, out, n, lc);
+}
+
+// ---------------------------------------------------------------------------- block scans
+// Inclusive Hillis-Steele scan of one fr per thread over a 256-thread block, operator `op`.
+// lds: 256*8 u32.
+template <class Op>
+__device__ __forceinline__ fr block_scan_incl(fr v, uint32_t* lds, Op op) {
+  const int t = threadIdx.x;
+  for (int off = 1; off < 256; off <<= 1) {
+    v.store(lds + 8 * t);
+    __syncthreads();
+    if (t >= off) v = op(fr::load(lds + 8 * (t - off)), v);
+    __syncthreads();
+  }
+  return v;
+}
+// inclusive suffix scan: result_t = op(v_t, op(v_{t+1}, ...))
+template <class Op>
+__device__ __forceinline__ fr block_suffix_incl(fr v, uint32_t* lds, Op op) {
+  const int t = threadIdx.x;
+  for (int off = 1; off < 256; off <<= 1) {
+    v.store(lds + 8 * t);
+    __syncthreads();
+    if (t + off < 256) v = op(v, fr::load(lds + 8 * (t + off)));
+    __syncthreads();
+  }
+  return v;
+}
+
+struct OpMul { __device__ fr operator()(const fr& a, const fr& b) const { return a * b; } };
+struct OpAdd { __device__ fr operator()(const fr& a, const fr& b) const { return a + b; } };
+
+// ---------------------------------------------------------------------------- builder
+// Element i of the input produces num_i/den_i stored at position (i+1) mod n.
+//  grand-sum  : f'=f+g, t'=t+g, num = t'*selF - f'*selT, den = f'*t'
+//  grand-prod : num = selF*(f+g-1)+1, den = selT*(t+g-1)+1
+template <bool PROD, bool SEL>
+__device__ __forceinline__ void numden(uint64_t i, const uint32_t* f, const uint32_t* t, const uint32_t* sf,
+                                       const uint32_t* stt, const fr& g, fr& num, fr& den) {
+  fr fv = fr::load(f + 8 * i) + g;
+  fr tv = fr::load(t + 8 * i) + g;
+  if (!PROD) {
+    if (SEL) {
+      num = tv * fr::load(sf + 8 * i) - fv * fr::load(stt + 8 * i);
+    } else {
+      num = tv - fv;
+    }
+    den = fv * tv;
+  } else {
+    if (SEL) {
+      const fr one = fr::one();
+      num = fr::load(sf + 8 * i) * (fv - one) + one;
+      den = fr::load(stt + 8 * i) * (tv - one) + one;
+    } else {
+      num = fv;
+      den = tv;
+    }
+  }
+}
+
+constexpr int BT_PER = 8;                 // elements per thread
+constexpr int BT_TILE = 256 * BT_PER;     // elements per tile (block)
+
+template <bool PROD, bool SEL>
+__global__ void __launch_bounds__(256) k_builder_tileprod(uint32_t* __restrict__ tileprod, const uint32_t* f,
+                                                          const uint32_t* t, const uint32_t* sf, const uint32_t* st_,
+                                                          const uint32_t* gp, uint64_t n) {
+  __shared__ uint32_t lds[256 * 8];
+  const fr g = fr::load(gp);
+  const uint64_t base = (uint64_t)blockIdx.x * BT_TILE + threadIdx.x * BT_PER;
+  fr p = fr::one();
+  for (int r = 0; r < BT_PER; r++) {
+    uint64_t i = base + r;
+    if (i < n) {
+      fr num, den;
+      numden<PROD, SEL>(i, f, t, sf, st_, g, num, den);
+      if (!den.is_zero()) p = p * den;
+    }
+  }
+  p = block_scan_incl(p, lds, OpMul());
+  if (threadIdx.x == 255) p.store(tileprod + 8 * (uint64_t)blockIdx.x);
+}
+
+// Single block: inverse of every tile product via prefix/suffix products and ONE inversion.
+__global__ void __launch_bounds__(1024) k_tile_inverse(uint32_t* __restrict__ tinv, const uint32_t* __restrict__ tp,
+                                                       uint32_t ntiles) {
+  __shared__ uint32_t lds[1024 * 8];
+  __shared__ uint32_t tot[8];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (ntiles + 1023) / 1024;
+  const uint32_t lo = t * per, hi = lo + per < ntiles ? lo + per : ntiles;
+  fr p = fr::one();
+  for (uint32_t b = lo; b < hi; b++) p = p * fr::load(tp + 8 * b);
+  // inclusive prefix over threads
+  fr pre = p;
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    pre.store(lds + 8 * t);
+    __syncthreads();
+    if (t >= off) pre = fr::load(lds + 8 * (t - off)) * pre;
+    __syncthreads();
+  }
+  fr suf = p;
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    suf.store(lds + 8 * t);
+    __syncthreads();
+    if (t + off < 1024) suf = suf * fr::load(lds + 8 * (t + off));
+    __syncthreads();
+  }
+  if (t == 1023) {
+    fr total_inv = pre.inverse();
+    total_inv.store(tot);
+  }
+  __syncthreads();
+  const fr total_inv = fr::load(tot);
+  // exclusive prefix / suffix of this thread's group
+  pre.store(lds + 8 * t);
+  __syncthreads();
+  fr pex = t ? fr::load(lds + 8 * (t - 1)) : fr::one();
+  __syncthreads();
+  suf.store(lds + 8 * t);
+  __syncthreads();
+  fr sex = t < 1023 ? fr::load(lds + 8 * (t + 1)) : fr::one();
+  // inverse of this thread's group product, then walk its tiles
+  fr ginv = total_inv * pex * sex;
+  // within group: inverse of tile b = ginv * (prod of other tiles in group)
+  // forward prefix in group then backward
+  fr run = fr::one();
+  for (uint32_t b = lo; b < hi; b++) {
+    run.store(tinv + 8 * b);  // prefix before b (temporary)
+    run = run * fr::load(tp + 8 * b);
+  }
+  fr acc = ginv;
+  for (uint32_t b = hi; b-- > lo;) {
+    fr prefix = fr::load(tinv + 8 * b);
+    fr inv_b = acc * prefix;
+    acc = acc * fr::load(tp + 8 * b);
+    inv_b.store(tinv + 8 * b);
+  }
+}
+
+// Per tile: element inverses (Montgomery trick seeded by the tile inverse), s_i = num_i/den_i,
+// local inclusive scan (sum or product) inside the tile, written to out[(i+1) mod n].
+template <bool PROD, bool SEL>
+__global__ void __launch_bounds__(256) k_builder_finish(uint32_t* __restrict__ out, uint32_t* __restrict__ tileacc,
+                                                        const uint32_t* __restrict__ tinv, const uint32_t* f,
+                                                        const uint32_t* t, const uint32_t* sf, const uint32_t* st_,
+                                                        const uint32_t* gp, uint64_t n) {
+  __shared__ uint32_t lds[256 * 8];
+  const fr g = fr::load(gp);
+  const uint64_t base = (uint64_t)blockIdx.x * BT_TILE + threadIdx.x * BT_PER;
+  fr num[BT_PER], den[BT_PER];
+  fr p = fr::one();
+#pragma unroll
+  for (int r = 0; r < BT_PER; r++) {
+    uint64_t i = base + r;
+    if (i < n) {
+      numden<PROD, SEL>(i, f, t, sf, st_, g, num[r], den[r]);
+    } else {
+      num[r] = PROD ? fr::one() : fr::zero();
+      den[r] = fr::one();
+    }
+    if (!den[r].is_zero()) p = p * den[r];
+  }
+  // exclusive prefix/suffix of thread products inside the tile
+  fr pin = block_scan_incl(p, lds, OpMul());
+  fr sin = block_suffix_incl(p, lds, OpMul());
+  pin.store(lds + 8 * threadIdx.x);
+  __syncthreads();
+  fr pex = threadIdx.x ? fr::load(lds + 8 * (threadIdx.x - 1)) : fr::one();
+  __syncthreads();
+  sin.store(lds + 8 * threadIdx.x);
+  __syncthreads();
+  fr sex = threadIdx.x < 255 ? fr::load(lds + 8 * (threadIdx.x + 1)) : fr::one();
+  __syncthreads();
+  fr inv = fr::load(tinv + 8 * (uint64_t)blockIdx.x) * pex * sex;  // 1/p
+  // backward: den_r^-1 = inv * prefix_{r-1}; recompute prefixes on the fly (store them in num? no:
+  // keep a small register array of prefixes)
+  fr pre[BT_PER];
+  fr run = fr::one();
+#pragma unroll
+  for (int r = 0; r < BT_PER; r++) {
+    pre[r] = run;
+    if (!den[r].is_zero()) run = run * den[r];
+  }
+  fr s[BT_PER];
+#pragma unroll
+  for (int r = BT_PER - 1; r >= 0; r--) {
+    if (den[r].is_zero()) {
+      s[r] = fr::zero();  // batchInverse(0) = 0 -> term 0
+      if (PROD) s[r] = fr::zero();
+    } else {
+      fr dinv = inv * pre[r];
+      inv = inv * den[r];
+      s[r] = num[r] * dinv;
+    }
+  }
+  // local inclusive scan inside thread, then across the tile
+  fr loc = s[0];
+#pragma unroll
+  for (int r = 1; r < BT_PER; r++) loc = PROD ? loc * s[r] : loc + s[r];
+  fr excl;
+  if (PROD) {
+    fr inc = block_scan_incl(loc, lds, OpMul());
+    inc.store(lds + 8 * threadIdx.x);
+    __syncthreads();
+    excl = threadIdx.x ? fr::load(lds + 8 * (threadIdx.x - 1)) : fr::one();
+    if (threadIdx.x == 255) inc.store(tileacc + 8 * (uint64_t)blockIdx.x);
+  } else {
+    fr inc = block_scan_incl(loc, lds, OpAdd());
+    inc.store(lds + 8 * threadIdx.x);
+    __syncthreads();
+    excl = threadIdx.x ? fr::load(lds + 8 * (threadIdx.x - 1)) : fr::zero();
+    if (threadIdx.x == 255) inc.store(tileacc + 8 * (uint64_t)blockIdx.x);
+  }
+  fr acc = excl;
+#pragma unroll
+  for (int r = 0; r < BT_PER; r++) {
+    uint64_t i = base + r;
+    acc = PROD ? acc * s[r] : acc + s[r];
+    if (i < n) {
+      uint64_t j = i + 1 == n ? 0 : i + 1;
+      acc.store(out + 8 * j);
+    }
+  }
+}
+
+// Single block: exclusive scan of tile accumulators -> carry per tile (in place).
+template <bool PROD>
+__global__ void __launch_bounds__(1024) k_tile_carry(uint32_t* __restrict__ acc, uint32_t ntiles) {
+  __shared__ uint32_t lds[1024 * 8];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (ntiles + 1023) / 1024;
+  const uint32_t lo = t * per, hi = lo + per < ntiles ? lo + per : ntiles;
+  fr s = PROD ? fr::one() : fr::zero();
+  for (uint32_t b = lo; b < hi; b++) s = PROD ? s * fr::load(acc + 8 * b) : s + fr::load(acc + 8 * b);
+  fr inc = s;
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    inc.store(lds + 8 * t);
+    __syncthreads();
+    if (t >= off) inc = PROD ? fr::load(lds + 8 * (t - off)) * inc : fr::load(lds + 8 * (t - off)) + inc;
+    __syncthreads();
+  }
+  inc.store(lds + 8 * t);
+  __syncthreads();
+  fr run = t ? fr::load(lds + 8 * (t - 1)) : (PROD ? fr::one() : fr::zero());
+  for (uint32_t b = lo; b < hi; b++) {
+    fr v = fr::load(acc + 8 * b);
+    run.store(acc + 8 * b);
+    run = PROD ? run * v : run + v;
+  }
+}
+
+// out[(i+1) mod n] (+|*)= carry[tile(i)]; flag if out[0] != (0 | 1)
+template <bool PROD>
+__global__ void k_apply_carry(uint32_t* __restrict__ out, const uint32_t* __restrict__ carry, uint64_t n,
+                              uint32_t* __restrict__ flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t tile = i / BT_TILE;
+  const uint64_t j = i + 1 == n ? 0 : i + 1;
+  fr v = fr::load(out + 8 * j);
+  if (tile) {
+    fr c = fr::load(carry + 8 * tile);
+    v = PROD ? v * c : v + c;
+    v.store(out + 8 * j);
+  }
+  if (j == 0) {
+    bool ok = PROD ? v == fr::one() : v.is_zero();
+    if (!ok) atomicOr(flag, 1u);
+  }
+}
+
+void launch_builder(hipStream_t st, bool prod, bool sel, uint32_t* out, const uint32_t* f, const uint32_t* t,
+                    const uint32_t* sf, const uint32_t* stt, const uint32_t* gamma, uint64_t n,
+                    uint32_t* scratch_tp, uint32_t* scratch_ti, uint32_t* flag) {
+  const uint32_t ntiles = (uint32_t)((n + BT_TILE - 1) / BT_TILE);
+#define KGS_BUILD(P, S)                                                                                      \
+  hipLaunchKernelGGL((k_builder_tileprod<P, S>), dim3(ntiles), dim3(256), 0, st, scratch_tp, f, t, sf, stt, gamma, n); \
+  hipLaunchKernelGGL(k_tile_inverse, dim3(1), dim3(1024), 0, st, scratch_ti, scratch_tp, ntiles);                   \
+  hipLaunchKernelGGL((k_builder_finish<P, S>), dim3(ntiles), dim3(256), 0, st, out, scratch_tp, scratch_ti, f, t, sf, \
+                     stt, gamma, n);                                                                                  \
+  hipLaunchKernelGGL((k_tile_carry<P>), dim3(1), dim3(1024), 0, st, scratch_tp, ntiles);                             \
+  hipLaunchKernelGGL((k_apply_carry<P>), dim3(nb(n)), dim3(256), 0, st, out, scratch_tp, n, flag);
+  if (prod) {
+    if (sel) { KGS_BUILD(true, true) } else { KGS_BUILD(true, false) }
+  } else {
+    if (sel) { KGS_BUILD(false, true) } else { KGS_BUILD(false, false) }
+  }
+#undef KGS_BUILD
+}
+
+// ---------------------------------------------------------------------------- quotient on a coset
+// Inputs: coset evaluations in bit-reversed order (size cs = 2^lcs) of S (or Z), F, T [, selF, selT].
+// rot = cs/n: S(w x_i) = S_eval[natural (i+rot) mod cs]. inv_nxm1[p] = 1/(n (x_i - 1)) (bitrev).
+// zinv[0|1] = 1/Z_H(x_i) for even/odd natural i (cs = 2n) or zinv[0] for all (cs = n).
+template <bool PROD, bool SEL>
+__global__ void __launch_bounds__(256) k_quotient(uint32_t* __restrict__ q, const uint32_t* __restrict__ S,
+                                                  const uint32_t* __restrict__ F, const uint32_t* __restrict__ T,
+                                                  const uint32_t* __restrict__ SF, const uint32_t* __restrict__ ST,
+                                                  const uint32_t* __restrict__ inv_nxm1, const uint32_t* __restrict__ sc,
+                                                  int lcs, uint32_t rot) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t cs = 1ull << lcs;
+  if (p >= cs) return;
+  // scalars: alpha, gamma, zinv0, zinv1
+  const fr alpha = fr::load(sc), gamma = fr::load(sc + 8), z0 = fr::load(sc + 16), z1 = fr::load(sc + 24);
+  const uint32_t i = brev((uint32_t)p, lcs);
+  const uint32_t j = (i + rot) & (uint32_t)(cs - 1);
+  const uint32_t pj = brev(j, lcs);
+  const fr s = fr::load(S + 8 * p), sw = fr::load(S + 8 * (uint64_t)pj);
+  const fr fg = fr::load(F + 8 * p) + gamma, tg = fr::load(T + 8 * p) + gamma;
+  fr acc = fr::zero();
+  fr sf, st;
+  if (SEL) {
+    sf = fr::load(SF + 8 * p);
+    st = fr::load(ST + 8 * p);
+    // alpha^3 (selT - selT^2) + alpha^2 (selF - selF^2)  ==  ((selT-selT^2)*alpha + (selF-selF^2))*alpha^2
+    acc = (st - st.sqr()) * alpha + (sf - sf.sqr());
+    acc = acc * alpha;  // will be multiplied by alpha once more below together with Q1
+  }
+  fr q1;
+  if (!PROD) {
+    q1 = (sw - s) * fg * tg;
+    if (SEL) q1 = q1 + st * fg - sf * tg;
+    else q1 = q1 + (fg - tg);  // F - T
+  } else {
+    const fr one = fr::one();
+    fr dT = tg, dF = fg;
+    if (SEL) {
+      dT = st * (tg - one) + one;
+      dF = sf * (fg - one) + one;
+    }
+    q1 = sw * dT - s * dF;
+  }
+  acc = (acc + q1) * alpha;
+  const fr zinv = (rot == 2 && (i & 1)) ? z1 : z0;
+  acc = acc * zinv;
+  // + L1(x) * S(x) / Z_H(x) = S(x) / (n (x-1))   (grand-product: (Z(x) - 1))
+  fr l = PROD ? (s - fr::one()) : s;
+  acc = acc + l * fr::load(inv_nxm1 + 8 * p);
+  acc.store(q + 8 * p);
+}
+
+void launch_quotient(hipStream_t st, bool prod, bool sel, uint32_t* q, const uint32_t* S, const uint32_t* F,
+                     const uint32_t* T, const uint32_t* SF, const uint32_t* ST, const uint32_t* inv_nxm1,
+                     const uint32_t* scalars, int lcs, uint32_t rot) {
+  uint64_t cs = 1ull << lcs;
+#define KGS_Q(P, S_)                                                                                          \
+  hipLaunchKernelGGL((k_quotient<P, S_>), dim3(nb(cs)), dim3(256), 0, st, q, S, F, T, SF, ST, inv_nxm1, scalars, lcs, rot);
+  if (prod) {
+    if (sel) { KGS_Q(true, true) } else { KGS_Q(true, false) }
+  } else {
+    if (sel) { KGS_Q(false, true) } else { KGS_Q(false, false) }
+  }
+#undef KGS_Q
+}
+
+// Divisibility of the quotient numerator by Z_H, evaluated on H (natural order): N(w^i) == 0.
+template <bool PROD, bool SEL>
+__global__ void k_divcheck(uint32_t* __restrict__ flag, const uint32_t* __restrict__ S, const uint32_t* __restrict__ f,
+                           const uint32_t* __restrict__ t, const uint32_t* __restrict__ sfp, const uint32_t* __restrict__ stp,
+                           const uint32_t* __restrict__ sc, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const fr alpha = fr::load(sc), gamma = fr::load(sc + 8);
+  const uint64_t j = i + 1 == n ? 0 : i + 1;
+  const fr s = fr::load(S + 8 * i), sw = fr::load(S + 8 * j);
+  const fr fg = fr::load(f + 8 * i) + gamma, tg = fr::load(t + 8 * i) + gamma;
+  fr acc = fr::zero(), sf, st;
+  if (SEL) {
+    sf = fr::load(sfp + 8 * i);
+    st = fr::load(stp + 8 * i);
+    acc = ((st - st.sqr()) * alpha + (sf - sf.sqr())) * alpha;
+  }
+  fr q1;
+  if (!PROD) {
+    q1 = (sw - s) * fg * tg;
+    if (SEL) q1 = q1 + st * fg - sf * tg;
+    else q1 = q1 + (fg - tg);
+  } else {
+    const fr one = fr::one();
+    fr dT = tg, dF = fg;
+    if (SEL) {
+      dT = st * (tg - one) + one;
+      dF = sf * (fg - one) + one;
+    }
+    q1 = sw * dT - s * dF;
+  }
+  acc = (acc + q1) * alpha;
+  if (i == 0) acc = acc + (PROD ? s - fr::one() : s);  // L1(w^0) = 1
+  if (!acc.is_zero()) atomicOr(flag, 1u);
+}
+
+void launch_divcheck(hipStream_t st, bool prod, bool sel, uint32_t* flag, const uint32_t* S, const uint32_t* f,
+                     const uint32_t* t, const uint32_t* sf, const uint32_t* stt, const uint32_t* scalars, uint64_t n) {
+#define KGS_D(P, S_) hipLaunchKernelGGL((k_divcheck<P, S_>), dim3(nb(n)), dim3(256), 0, st, flag, S, f, t, sf, stt, scalars, n);
+  if (prod) {
+    if (sel) { KGS_D(true, true) } else { KGS_D(true, false) }
+  } else {
+    if (sel) { KGS_D(false, true) } else { KGS_D(false, false) }
+  }
+#undef KGS_D
+}
+
+// ---------------------------------------------------------------------------- Horner tiles
+// part[poly][tile] = sum_{j in tile} c_j x^(j - tile_start); tile = 2048 coefficients.
+// xp[l] = x^(8 * 2^l), l = 0..7 ; x itself at xp[8]
+__global__ void __launch_bounds__(256) k_eval_tiles(uint32_t* __restrict__ part, EvalBatch eb,
+                                                    const uint32_t* __restrict__ xp, uint32_t ntiles_max) {
+  __shared__ uint32_t lds[256 * 8];
+  const int pi = blockIdx.y;
+  const uint32_t* c = eb.src[pi];
+  const uint64_t len = eb.len[pi];
+  const uint64_t base = (uint64_t)blockIdx.x * BT_TILE + threadIdx.x * BT_PER;
+  const fr x = fr::load(xp + 8 * 8);
+  fr h = fr::zero();
+#pragma unroll
+  for (int r = BT_PER - 1; r >= 0; r--) {
+    uint64_t i = base + r;
+    fr ci = i < len ? fr::load(c + 8 * i) : fr::zero();
+    h = h * x + ci;
+  }
+  // tree: thread t (multiple of 2^(l+1)) absorbs t + 2^l scaled by x^(8*2^l)
+  for (int l = 0; l < 8; l++) {
+    h.store(lds + 8 * threadIdx.x);
+    __syncthreads();
+    const int span = 1 << l;
+    if ((threadIdx.x & (2 * span - 1)) == 0) h = h + fr::load(lds + 8 * (threadIdx.x + span)) * fr::load(xp + 8 * l);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) h.store(part + 8 * ((uint64_t)pi * ntiles_max + blockIdx.x));
+}
+
+void launch_eval_tiles(hipStream_t st, uint32_t* part, const EvalBatch& eb, const uint32_t* xp, uint32_t ntiles_max) {
+  hipLaunchKernelGGL(k_eval_tiles, dim3(ntiles_max, eb.npolys), dim3(256), 0, st, part, eb, xp, ntiles_max);
+}
+
+// ---------------------------------------------------------------------------- synthetic division
+// r_i = a_i + z r_{i+1} (r_L = 0); quotient q_{i-1} = r_i; r_0 must be 0.
+// tile carries: carry[b] = r_{start of tile b+1}, from tile Horner values h_b (part) with Z = z^2048.
+__global__ void __launch_bounds__(1024) k_div_carries(uint32_t* __restrict__ carry, const uint32_t* __restrict__ h,
+                                                      uint32_t ntiles, const uint32_t* __restrict__ zT) {
+  __shared__ uint32_t lds[1024 * 8];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (ntiles + 1023) / 1024;
+  const uint32_t lo = t * per, hi = lo + per < ntiles ? lo + per : ntiles;
+  const fr Z = fr::load(zT);
+  // group value: sum_{b in [lo,hi)} h_b Z^(b-lo), and Z^(hi-lo)
+  fr v = fr::zero(), zp = fr::one();
+  for (uint32_t b = hi; b-- > lo;) v = v * Z + fr::load(h + 8 * b);
+  for (uint32_t b = lo; b < hi; b++) zp = zp * Z;
+  // suffix scan over groups: V_t = v_t + zp_t * V_{t+1}; multipliers compose by product
+  fr V = v, M = zp;
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    V.store(lds + 8 * t);
+    __syncthreads();
+    fr Vn = t + off < 1024 ? fr::load(lds + 8 * (t + off)) : fr::zero();
+    __syncthreads();
+    M.store(lds + 8 * t);
+    __syncthreads();
+    fr Mn = t + off < 1024 ? fr::load(lds + 8 * (t + off)) : fr::one();
+    __syncthreads();
+    V = V + M * Vn;
+    M = M * Mn;
+  }
+  // V is now the inclusive suffix value at group start lo; carry-in for this group = V_{t+1}
+  V.store(lds + 8 * t);
+  __syncthreads();
+  fr cin = t + 1 < 1024 ? fr::load(lds + 8 * (t + 1)) : fr::zero();
+  for (uint32_t b = hi; b-- > lo;) {
+    cin.store(carry + 8 * b);                 // r at start of tile b+1
+    cin = fr::load(h + 8 * b) + Z * cin;      // r at start of tile b
+  }
+}
+
+// xp layout (shared with k_eval_tiles): xp[l] = z^(8*2^l) (l = 0..7), xp[8] = z, xp[9] = z^2048.
+__global__ void __launch_bounds__(256) k_div_finish(uint32_t* __restrict__ q, uint32_t* __restrict__ flag,
+                                                    const uint32_t* __restrict__ a, uint64_t L,
+                                                    const uint32_t* __restrict__ carry, const uint32_t* __restrict__ xp) {
+  __shared__ uint32_t lds[256 * 8];
+  const fr z = fr::load(xp + 8 * 8);
+  const uint64_t base = (uint64_t)blockIdx.x * BT_TILE + threadIdx.x * BT_PER;
+  fr av[BT_PER];
+  fr h = fr::zero();
+#pragma unroll
+  for (int r = BT_PER - 1; r >= 0; r--) {
+    uint64_t i = base + r;
+    av[r] = i < L ? fr::load(a + 8 * i) : fr::zero();
+    h = h * z + av[r];
+  }
+  const fr cin_tile = fr::load(carry + 8 * (uint64_t)blockIdx.x);
+  if (threadIdx.x == 255) h = h + fr::load(xp) * cin_tile;  // z^8 * carry
+  // inclusive suffix scan: V_t = h_t + z^8 V_{t+1}; at step l the multiplier is z^(8*2^l)
+  for (int l = 0; l < 8; l++) {
+    const int off = 1 << l;
+    h.store(lds + 8 * threadIdx.x);
+    __syncthreads();
+    if (threadIdx.x + off < 256) h = h + fr::load(xp + 8 * l) * fr::load(lds + 8 * (threadIdx.x + off));
+    __syncthreads();
+  }
+  h.store(lds + 8 * threadIdx.x);
+  __syncthreads();
+  fr r = threadIdx.x < 255 ? fr::load(lds + 8 * (threadIdx.x + 1)) : cin_tile;
+#pragma unroll
+  for (int k = BT_PER - 1; k >= 0; k--) {
+    uint64_t i = base + k;
+    r = av[k] + z * r;  // r_i
+    if (i < L) {
+      if (i >= 1) r.store(q + 8 * (i - 1));
+      else if (!r.is_zero()) atomicOr(flag, 1u);
+    }
+  }
+}
+
+void launch_divide(hipStream_t st, uint32_t* q, uint32_t* flag, const uint32_t* a, uint64_t L, const uint32_t* xp,
+                   uint32_t* part, uint32_t* carry) {
+  const uint32_t ntiles = (uint32_t)((L + BT_TILE - 1) / BT_TILE);
+  EvalBatch eb;
+  eb.npolys = 1;
+  eb.src[0] = a;
+  eb.len[0] = L;
+  hipMemsetAsync(q + 8 * (L - 1), 0, 32, st);
+  hipLaunchKernelGGL(k_eval_tiles, dim3(ntiles, 1), dim3(256), 0, st, part, eb, xp, ntiles);
+  hipLaunchKernelGGL(k_div_carries, dim3(1), dim3(1024), 0, st, carry, part, ntiles, xp + 8 * 9);
+  hipLaunchKernelGGL(k_div_finish, dim3(ntiles), dim3(256), 0, st, q, flag, a, L, carry, xp);
+}
+
+// ---------------------------------------------------------------------------- Fr batch inverse
+// out[i] = in[i]^-1 (0 -> 0), per-thread Montgomery trick over CH elements (domain setup only).
+__global__ void k_fr_batch_inv(uint32_t* __restrict__ out, const uint32_t* __restrict__ in, uint64_t n, uint32_t ch) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t start = t * ch;
+  if (start >= n) return;
+  const uint64_t end = start + ch < n ? start + ch : n;
+  fr acc = fr::one();
+  for (uint64_t i = start; i < end; i++) {
+    acc.store(out + 8 * i);
+    fr v = fr::load(in + 8 * i);
+    if (!v.is_zero()) acc = acc * v;
+  }
+  fr inv = acc.inverse();
+  for (uint64_t i = end; i-- > start;) {
+    fr v = fr::load(in + 8 * i);
+    if (v.is_zero()) { fr::zero().store(out + 8 * i); continue; }
+    fr pre = fr::load(out + 8 * i);
+    (inv * pre).store(out + 8 * i);
+    inv = inv * v;
+  }
+}
+void launch_fr_batch_inv(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t n) {
+  const uint32_t ch = 32;
+  hipLaunchKernelGGL(k_fr_batch_inv, dim3(nb((n + ch - 1) / ch)), dim3(256), 0, st, out, in, n, ch);
+}
+
+// x_i = g w_cs^i (natural) -> n (x_i - 1) stored at bitrev position (domain setup only).
+// tw holds w_M^j for j < M/2; w_M^(j + M/2) = -w_M^j.
+__global__ void k_nxm1(uint32_t* __restrict__ out, const uint32_t* __restrict__ tw, uint64_t halfM,
+                       const uint32_t* __restrict__ gp, const uint32_t* __restrict__ np, int lcs, uint64_t wstride) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (1ull << lcs)) return;
+  uint64_t e = i * wstride;
+  fr w = e < halfM ? fr::load(tw + 8 * e) : fr::load(tw + 8 * (e - halfM)).neg();
+  fr x = fr::load(gp) * w;
+  fr v = fr::load(np) * (x - fr::one());
+  v.store(out + 8 * (uint64_t)brev((uint32_t)i, lcs));
+}
+void launch_nxm1(hipStream_t st, uint32_t* out, const uint32_t* tw, uint64_t halfM, const uint32_t* gp,
+                 const uint32_t* np, int lcs, uint64_t wstride) {
+  hipLaunchKernelGGL(k_nxm1, dim3(nb(1ull << lcs)), dim3(256), 0, st, out, tw, halfM, gp, np, lcs, wstride);
+}
+
+}  // namespace kgs

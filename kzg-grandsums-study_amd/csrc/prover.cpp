@@ -1,0 +1,1262 @@
+// Host orchestration of the MI355X-native grand-sum / grand-product KZG prover + the C-ABI
+// (include/kgs.h). One context = one device, one HIP stream, a device-resident SRS with its MSM
+// window tables, NTT/coset tables, and a grow-only device buffer pool.
+//
+// Round structure, transcript order and proof schema follow the reference provers exactly
+// (src/grandsum/mset_eq_kzg_prover.js:12-434, src/grandproduct/mset_eq_kzg_prover.js:12-414).
+// Every output is a unique field / group element, so the computation is re-planned for the GPU
+// where that leaves the values unchanged (DESIGN.md §Hot path):
+//  * evalsF = fft(sum beta^i F_i) = sum beta^i f_i (NTT linearity; prover.js:207-217)
+//  * the quotient Q = N / Z_H is computed on a coset of size 2n (n for the unselected grand
+//    product) instead of the 2n/4n `multiply` chain + `divZh` (prover.js:233-286); divisibility
+//    (the "Polynomial is not divisible" check of divZh) is decided exactly by N(w^i) == 0 on H;
+//  * S(wX) on the coset is a rotation of the coset evaluations (no shiftOmega NTT pair);
+//  * L1(X)/Z_H(X) = 1/(n (X - 1)) on the coset (precomputed per domain);
+//  * commitments skip zero top coefficients by degree bounds (zero scalars add nothing).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <chrono>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/kgs.h"
+#include "host_field.hpp"
+#include "kernels.hpp"
+#include "keccak.hpp"
+
+using namespace kgs;
+using host::Fq;
+using host::Fr;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct KgsError : std::runtime_error {
+  int code;
+  KgsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HC(x)                                                                                    \
+  do {                                                                                           \
+    hipError_t e_ = (x);                                                                         \
+    if (e_ != hipSuccess)                                                                        \
+      throw KgsError(KGS_E_HIP, std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x); \
+  } while (0)
+
+static void check_launch() {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw KgsError(KGS_E_HIP, std::string("HIP launch error: ") + hipGetErrorString(e));
+}
+
+// ------------------------------------------------------------------ constants
+// Fr.w[k] (standard BN254 roots: nqr = 5, s = 28) and the coset shift g = 5
+static Fr fr_w(int k) {
+  // (r-1) >> 28
+  uint64_t e[4];
+  memcpy(e, host::FR_MOD.p, 32);
+  e[0] -= 1;
+  for (int s = 0; s < 28; s++) {
+    e[0] = (e[0] >> 1) | (e[1] << 63);
+    e[1] = (e[1] >> 1) | (e[2] << 63);
+    e[2] = (e[2] >> 1) | (e[3] << 63);
+    e[3] >>= 1;
+  }
+  Fr w = Fr::from_u64(5).pow(e);
+  for (int s = 28; s > k; s--) w = w.sqr();
+  return w;
+}
+
+struct DBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct Transcript {
+  std::vector<uint8_t> buf;
+  void add_commitment(const uint8_t lem[64]) {
+    uint8_t rpr[64];
+    host::g1_lem_to_rpr_uncompressed(lem, rpr);
+    buf.insert(buf.end(), rpr, rpr + 64);
+  }
+  void add_scalar(const Fr& s) {
+    uint8_t be[32];
+    s.to_be_std(be);
+    buf.insert(buf.end(), be, be + 32);
+  }
+  Fr challenge() const {
+    uint8_t h[32];
+    host::keccak256(buf.data(), buf.size(), h);
+    return Fr::from_be_reduce(h);
+  }
+};
+
+}  // namespace
+
+struct kgs_ctx {
+  int device = 0;
+  hipStream_t st = nullptr;
+  std::map<std::string, DBuf> pool;
+  // pinned staging
+  uint8_t* h_pin = nullptr;
+  size_t h_pin_bytes = 0;
+  size_t h_pin_off = 0;
+  uint32_t* d_scal = nullptr;  // device scalar area
+  size_t d_scal_off = 0;
+  static constexpr size_t SCAL_BYTES = 1 << 16;
+  // SRS
+  std::string srs_key;
+  int srs_power = -1;
+  int nbits_max = -1;
+  MsmTables tb;
+  MsmWork mw;
+  uint64_t msm_nseg_max = 0;
+  // domain tables (M = 2^logM)
+  int logM = -1;
+  uint32_t *tw_fwd = nullptr, *tw_inv = nullptr, *coset_pow = nullptr, *coset_ipow = nullptr, *invm = nullptr;
+  std::map<std::pair<int, int>, uint32_t*> nxm1;  // (nbits, lcs) -> 1/(n(x-1)) on the coset (bitrev)
+  std::vector<double> timing;
+
+  ~kgs_ctx() {
+    hipSetDevice(device);
+    if (st) hipStreamSynchronize(st);
+    for (auto& kv : pool) hipFree(kv.second.p);
+    if (h_pin) hipHostFree(h_pin);
+    if (st) hipStreamDestroy(st);
+  }
+
+  uint32_t* buf(const std::string& name, size_t bytes) {
+    DBuf& b = pool[name];
+    if (b.bytes < bytes) {
+      if (b.p) {
+        HC(hipStreamSynchronize(st));
+        HC(hipFree(b.p));
+        b.p = nullptr;
+      }
+      HC(hipMalloc(&b.p, bytes < 64 ? 64 : bytes));
+      b.bytes = bytes < 64 ? 64 : bytes;
+    }
+    return (uint32_t*)b.p;
+  }
+  void ensure_pin(size_t bytes) {
+    if (h_pin_bytes >= bytes) return;
+    if (h_pin) {
+      HC(hipStreamSynchronize(st));
+      HC(hipHostFree(h_pin));
+    }
+    HC(hipHostMalloc((void**)&h_pin, bytes, hipHostMallocDefault));
+    h_pin_bytes = bytes;
+  }
+  // bump-allocated pinned region (valid until reset_staging(), i.e. until the next sync point)
+  uint8_t* pin(size_t bytes) {
+    bytes = (bytes + 63) & ~size_t(63);
+    if (h_pin_off + bytes > h_pin_bytes) throw KgsError(KGS_E_ARG, "pinned staging exhausted");
+    uint8_t* p = h_pin + h_pin_off;
+    h_pin_off += bytes;
+    return p;
+  }
+  // copy host scalars to the device scalar area; returns the device pointer
+  uint32_t* scal(const Fr* v, int count) {
+    size_t bytes = 32 * (size_t)count;
+    if (d_scal_off + bytes > SCAL_BYTES) throw KgsError(KGS_E_ARG, "scalar staging exhausted");
+    uint8_t* h = pin(bytes);
+    for (int i = 0; i < count; i++) v[i].to_bytes(h + 32 * i);
+    uint32_t* d = d_scal + d_scal_off / 4;
+    d_scal_off += bytes;
+    HC(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
+    return d;
+  }
+  void sync() { HC(hipStreamSynchronize(st)); }
+  void reset_staging() {
+    sync();
+    h_pin_off = 0;
+    d_scal_off = 0;
+  }
+};
+
+namespace {
+
+// ------------------------------------------------------------------ domain tables
+void ensure_domain(kgs_ctx& c, int logM) {
+  if (c.logM >= logM) return;
+  const uint64_t M = 1ull << logM;
+  c.tw_fwd = c.buf("tw_fwd", 32 * (M / 2 ? M / 2 : 1));
+  c.tw_inv = c.buf("tw_inv", 32 * (M / 2 ? M / 2 : 1));
+  c.coset_pow = c.buf("coset_pow", 32 * M);
+  c.coset_ipow = c.buf("coset_ipow", 32 * M);
+  c.invm = c.buf("invm", 32 * (logM + 1));
+  c.reset_staging();
+  Fr w = fr_w(logM), wi = w.inverse();
+  Fr g = Fr::from_u64(5), gi = g.inverse();
+  Fr consts[4] = {w, wi, g, gi};
+  uint32_t* d = c.scal(consts, 4);
+  if (M / 2) {
+    launch_powers(c.st, c.tw_fwd, M / 2, d, nullptr);
+    launch_powers(c.st, c.tw_inv, M / 2, d + 8, nullptr);
+  }
+  launch_powers(c.st, c.coset_pow, M, d + 16, nullptr);
+  launch_powers(c.st, c.coset_ipow, M, d + 24, nullptr);
+  std::vector<Fr> im(logM + 1);
+  for (int l = 0; l <= logM; l++) im[l] = Fr::from_u64(1ull << l).inverse();
+  uint8_t* h = c.pin(32 * (logM + 1));
+  for (int l = 0; l <= logM; l++) im[l].to_bytes(h + 32 * l);
+  HC(hipMemcpyAsync(c.invm, h, 32 * (logM + 1), hipMemcpyHostToDevice, c.st));
+  check_launch();
+  c.reset_staging();
+  for (auto& kv : c.nxm1) (void)kv;  // tables depend only on (nbits, lcs) and M-stride: rebuild lazily
+  c.nxm1.clear();
+  c.logM = logM;
+}
+
+uint32_t* get_nxm1(kgs_ctx& c, int nbits, int lcs) {
+  auto key = std::make_pair(nbits, lcs);
+  auto it = c.nxm1.find(key);
+  if (it != c.nxm1.end()) return it->second;
+  const uint64_t cs = 1ull << lcs;
+  uint32_t* out = c.buf("nxm1_" + std::to_string(nbits) + "_" + std::to_string(lcs), 32 * cs);
+  uint32_t* tmp = c.buf("nxm1_tmp", 32 * cs);
+  Fr consts[2] = {Fr::from_u64(5), Fr::from_u64(1ull << nbits)};
+  uint32_t* d = c.scal(consts, 2);
+  launch_nxm1(c.st, tmp, c.tw_fwd, (1ull << c.logM) / 2, d, d + 8, lcs, (1ull << c.logM) >> lcs);
+  launch_fr_batch_inv(c.st, out, tmp, cs);
+  check_launch();
+  c.nxm1[key] = out;
+  return out;
+}
+
+// ------------------------------------------------------------------ NTT helpers
+// natural-order evaluations -> natural-order coefficients (out != in)
+void intt_nat(kgs_ctx& c, uint32_t* out, const uint32_t* in, int logm) {
+  ntt_dit(c.st, out, in, 0, logm, c.tw_inv, c.logM, nullptr, c.invm + 8 * logm);
+}
+// coefficients (len <= 2^lcs, natural) -> coset evaluations p(g w^i), bit-reversed order
+void coset_fwd(kgs_ctx& c, uint32_t* out, const uint32_t* in, uint64_t len, int lcs) {
+  ntt_dif(c.st, out, in, len, lcs, c.coset_pow, c.tw_fwd, c.logM);
+}
+// bit-reversed coset evaluations -> natural coefficients (in place allowed)
+void coset_inv(kgs_ctx& c, uint32_t* out, const uint32_t* in, int lcs) {
+  ntt_dit(c.st, out, in, 1, lcs, c.tw_inv, c.logM, c.coset_ipow, c.invm + 8 * lcs);
+}
+
+// ------------------------------------------------------------------ SRS
+int choose_c(uint64_t npts) {
+  int lg = 0;
+  while ((1ull << lg) < npts) lg++;
+  int cc = lg - 4;
+  if (cc < 6) cc = 6;
+  if (cc > 16) cc = 16;
+  return cc;
+}
+
+void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int nbits_max, const std::string& key) {
+  if (npts < 2) throw KgsError(KGS_E_ARG, "SRS needs at least 2 points");
+  c.sync();
+  const int cc = choose_c(npts);
+  const int W = (255 + cc - 1) / cc;
+  c.tb.npts = npts;
+  c.tb.c = cc;
+  c.tb.W = W;
+  c.tb.table = c.buf("msm_table", (size_t)W * npts * 64);
+  HC(hipMemcpy(c.tb.table, lem, npts * 64, hipMemcpyHostToDevice));
+  uint32_t* tmp = c.buf("msm_tmp_xyzz", npts * 128);
+  uint32_t* scr = c.buf("msm_tmp_scr", npts * 32);
+  msm_build_table(c.st, c.tb.table, npts, cc, W, tmp, scr);
+  check_launch();
+  // work buffers for N <= npts
+  const uint64_t E = npts * W;
+  const uint32_t B = 1u << (cc - 1);
+  uint64_t nseg = (1ull << 18) + (1ull << 16) + 2;
+  if (E / 64 + 2 > nseg) nseg = E / 64 + 2;
+  c.msm_nseg_max = nseg;
+  c.mw.digit = (int32_t*)c.buf("msm_digit", E * 4);
+  c.mw.sorted = c.buf("msm_sorted", E * 4);
+  c.mw.counts = c.buf("msm_counts", 4 * (B + 4));
+  c.mw.offsets = c.buf("msm_offsets", 4 * (B + 4));
+  c.mw.cursor = c.buf("msm_cursor", 4 * (B + 4));
+  c.mw.bstart = c.buf("msm_bstart", 128 * (size_t)(B + 2));
+  c.mw.segpart = c.buf("msm_segpart", 128 * nseg);
+  c.mw.buckets = c.buf("msm_buckets", 128 * (size_t)(B + 2));
+  const uint32_t chunks = (B / 2 + 255) / 256 > 0 ? (B / 2 + 255) / 256 : 1;
+  c.mw.part = c.buf("msm_part", 128 * (size_t)cc * chunks);
+  c.srs_power = power;
+  c.nbits_max = nbits_max;
+  ensure_domain(c, nbits_max + 1);
+  c.sync();
+  c.srs_key = key;
+}
+
+// ------------------------------------------------------------------ MSM (commit)
+struct Commit {
+  uint8_t* h_T = nullptr;  // pinned, c x 128 B
+  uint64_t N = 0;
+};
+
+Commit commit_launch(kgs_ctx& c, const uint32_t* scalars, uint64_t N, int slot) {
+  Commit cm;
+  cm.N = N;
+  const int cc = c.tb.c;
+  uint32_t* dT = c.buf("msm_T", (size_t)64 * cc * 128) + (size_t)slot * cc * 32;
+  if (N > c.tb.npts) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
+  cm.h_T = c.pin((size_t)cc * 128);
+  if (N == 0) {
+    memset(cm.h_T, 0, (size_t)cc * 128);
+    return cm;
+  }
+  msm_run(c.st, c.tb, c.mw, scalars, N, dT);
+  check_launch();
+  HC(hipMemcpyAsync(cm.h_T, dT, (size_t)cc * 128, hipMemcpyDeviceToHost, c.st));
+  return cm;
+}
+
+// after sync: sum_k 2^k T_k -> affine LEM
+void commit_finish(kgs_ctx& c, const Commit& cm, uint8_t out[64]) {
+  const int cc = c.tb.c;
+  host::G1 acc = host::G1::inf();
+  if (cm.N) {
+    for (int k = cc - 1; k >= 0; k--) {
+      acc = acc.dbl();
+      acc = acc.add(host::G1::from_bytes128(cm.h_T + 128 * k));
+    }
+  }
+  acc.to_affine_lem(out);
+}
+
+// ------------------------------------------------------------------ Horner evaluation
+// returns p_j(x) for each poly of the batch
+struct EvalJob {
+  std::vector<const uint32_t*> src;
+  std::vector<uint64_t> len;
+  uint8_t* h_part = nullptr;
+  uint32_t ntiles = 0;
+  Fr x;
+};
+
+uint32_t* xpowers(kgs_ctx& c, const Fr& x) {
+  Fr p[10];
+  Fr x8 = x.sqr().sqr().sqr();
+  p[0] = x8;
+  for (int l = 1; l < 8; l++) p[l] = p[l - 1].sqr();
+  p[8] = x;
+  p[9] = p[7].sqr();  // x^2048
+  return c.scal(p, 10);
+}
+
+EvalJob eval_launch(kgs_ctx& c, const std::vector<const uint32_t*>& src, const std::vector<uint64_t>& len, const Fr& x,
+                    int slot) {
+  EvalJob j;
+  j.src = src;
+  j.len = len;
+  j.x = x;
+  uint64_t maxlen = 1;
+  for (auto l : len) maxlen = l > maxlen ? l : maxlen;
+  j.ntiles = (uint32_t)((maxlen + EVAL_TILE - 1) / EVAL_TILE);
+  EvalBatch eb;
+  eb.npolys = (int)src.size();
+  if (eb.npolys > EB_MAX) throw KgsError(KGS_E_ARG, "too many polynomials in one evaluation batch");
+  for (int i = 0; i < eb.npolys; i++) {
+    eb.src[i] = src[i];
+    eb.len[i] = len[i];
+  }
+  uint32_t* xp = xpowers(c, x);
+  size_t bytes = (size_t)32 * j.ntiles * eb.npolys;
+  uint32_t* dpart = c.buf("eval_part_" + std::to_string(slot), bytes);
+  launch_eval_tiles(c.st, dpart, eb, xp, j.ntiles);
+  check_launch();
+  j.h_part = c.pin(bytes);
+  HC(hipMemcpyAsync(j.h_part, dpart, bytes, hipMemcpyDeviceToHost, c.st));
+  return j;
+}
+
+std::vector<Fr> eval_finish(const EvalJob& j) {
+  Fr X = j.x;
+  for (int i = 0; i < 11; i++) X = X.sqr();  // x^2048
+  std::vector<Fr> out;
+  for (size_t p = 0; p < j.src.size(); p++) {
+    Fr v = Fr::zero();
+    for (uint32_t b = j.ntiles; b-- > 0;) v = v * X + Fr::from_bytes(j.h_part + 32 * ((size_t)p * j.ntiles + b));
+    out.push_back(v);
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------ the prover
+struct ProveIn {
+  int kind, nbits, npols;
+  std::vector<const uint32_t*> f_std, t_std;  // device, standard form
+  const uint32_t *sel_f = nullptr, *sel_t = nullptr;  // device, Montgomery (nullptr: unselected)
+  std::vector<uint8_t*> mont_f_out, mont_t_out;  // host outputs (may be empty)
+};
+
+void set_lc_term(LinComb& lc, const uint32_t* src, uint64_t len, const Fr& coef) {
+  if (lc.nterms >= LC_MAX) throw KgsError(KGS_E_ARG, "too many linear-combination terms");
+  lc.src[lc.nterms] = src;
+  lc.len[lc.nterms] = len;
+  coef.to_bytes((uint8_t*)lc.coef[lc.nterms]);
+  lc.nterms++;
+}
+
+void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out) {
+  using clk = std::chrono::steady_clock;
+  auto t0 = clk::now();
+  c.timing.assign(6, 0.0);
+  auto lap = [&](int r) {
+    auto t1 = clk::now();
+    c.timing[r] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    t0 = t1;
+  };
+  const bool gs = in.kind == KGS_GRANDSUM;
+  const bool sel = in.sel_f != nullptr;
+  const int k = in.npols;
+  const int nbits = in.nbits;
+  const uint64_t n = 1ull << nbits;
+  const size_t E = 32 * n;
+  if (nbits < 1) throw KgsError(KGS_E_ARG, "nbits must be >= 1");
+  if (c.srs_power < 0) throw KgsError(KGS_E_ARG, "no SRS loaded");
+  if (c.srs_power < nbits)
+    throw KgsError(KGS_E_SRS, "The Powers of Tau file is not sufficiently large to commit the polynomials.");
+  if (nbits > c.nbits_max) throw KgsError(KGS_E_SRS, "SRS loaded for a smaller maximum domain; reload with larger nbits_max");
+  if (k < 1) throw KgsError(KGS_E_ARG, "The number of multisets must be greater than 0.");
+  if (k > 10) throw KgsError(KGS_E_ARG, "at most 10 multisets per proof are supported");
+  c.reset_staging();
+  uint32_t* flags = c.buf("flags", 64);
+  HC(hipMemsetAsync(flags, 0, 64, c.st));
+  const bool vec = k > 1;
+
+  // ---------------- round 1: witness polynomials + commitments (prover.js:144-179)
+  std::vector<uint32_t*> fm(k), tm(k), Fc(k), Tc(k);
+  for (int i = 0; i < k; i++) {
+    fm[i] = c.buf("fm" + std::to_string(i), E);
+    tm[i] = c.buf("tm" + std::to_string(i), E);
+    Fc[i] = c.buf("Fc" + std::to_string(i), E);
+    Tc[i] = c.buf("Tc" + std::to_string(i), E);
+    launch_to_mont(c.st, fm[i], in.f_std[i], n);
+    launch_to_mont(c.st, tm[i], in.t_std[i], n);
+    intt_nat(c, Fc[i], fm[i], nbits);
+    intt_nat(c, Tc[i], tm[i], nbits);
+  }
+  check_launch();
+  for (int i = 0; i < k; i++) {
+    if (!in.mont_f_out.empty() && in.mont_f_out[i]) HC(hipMemcpyAsync(in.mont_f_out[i], fm[i], E, hipMemcpyDeviceToHost, c.st));
+    if (!in.mont_t_out.empty() && in.mont_t_out[i]) HC(hipMemcpyAsync(in.mont_t_out[i], tm[i], E, hipMemcpyDeviceToHost, c.st));
+  }
+  uint32_t *sFc = nullptr, *sTc = nullptr;
+  if (sel) {
+    sFc = c.buf("sFc", E);
+    sTc = c.buf("sTc", E);
+    intt_nat(c, sFc, in.sel_f, nbits);
+    intt_nat(c, sTc, in.sel_t, nbits);
+  }
+  std::vector<Commit> r1;
+  int slot = 0;
+  for (int i = 0; i < k; i++) {
+    r1.push_back(commit_launch(c, Fc[i], n, slot++));
+    r1.push_back(commit_launch(c, Tc[i], n, slot++));
+  }
+  if (sel) {
+    r1.push_back(commit_launch(c, sFc, n, slot++));
+    r1.push_back(commit_launch(c, sTc, n, slot++));
+  }
+  c.sync();
+  const int ncom = 2 * k + (sel ? 2 : 0) + 4;
+  std::vector<std::vector<uint8_t>> com(ncom, std::vector<uint8_t>(64));
+  int ci = 0;
+  for (auto& cm : r1) commit_finish(c, cm, com[ci++].data());
+  lap(0);
+
+  // ---------------- round 2: challenges, combined polynomials, S / Z (prover.js:181-231)
+  Transcript tr;
+  for (int i = 0; i < ci; i++) tr.add_commitment(com[i].data());
+  Fr beta = Fr::zero();
+  if (vec) {
+    beta = tr.challenge();
+    tr.add_scalar(beta);
+  }
+  const Fr gamma = tr.challenge();
+  std::vector<Fr> bpow(k);
+  bpow[0] = Fr::one();
+  for (int i = 1; i < k; i++) bpow[i] = bpow[i - 1] * beta;
+  const uint32_t *fcomb = fm[0], *tcomb = tm[0], *polF = Fc[0], *polT = Tc[0];
+  if (vec) {
+    uint32_t* b_fe = c.buf("fcomb", E);
+    uint32_t* b_te = c.buf("tcomb", E);
+    uint32_t* b_F = c.buf("polF", E);
+    uint32_t* b_T = c.buf("polT", E);
+    LinComb l1{}, l2{}, l3{}, l4{};
+    for (int i = 0; i < k; i++) {
+      set_lc_term(l1, fm[i], n, bpow[i]);
+      set_lc_term(l2, tm[i], n, bpow[i]);
+      set_lc_term(l3, Fc[i], n, bpow[i]);
+      set_lc_term(l4, Tc[i], n, bpow[i]);
+    }
+    launch_lincomb(c.st, b_fe, n, l1);
+    launch_lincomb(c.st, b_te, n, l2);
+    launch_lincomb(c.st, b_F, n, l3);
+    launch_lincomb(c.st, b_T, n, l4);
+    fcomb = b_fe;
+    tcomb = b_te;
+    polF = b_F;
+    polT = b_T;
+  }
+  uint32_t* Sev = c.buf("Sev", E);
+  uint32_t* Sc = c.buf("Sc", E);
+  const uint32_t ntiles = (uint32_t)((n + EVAL_TILE - 1) / EVAL_TILE);
+  uint32_t* d_gamma = c.scal(&gamma, 1);
+  launch_builder(c.st, !gs, sel, Sev, fcomb, tcomb, in.sel_f, in.sel_t, d_gamma, n, c.buf("bt_tp", 32 * (ntiles + 1)),
+                 c.buf("bt_ti", 32 * (ntiles + 1)), flags);
+  intt_nat(c, Sc, Sev, nbits);
+  check_launch();
+  Commit cS = commit_launch(c, Sc, n, slot++);
+  uint32_t* h_flags = (uint32_t*)c.pin(64);
+  HC(hipMemcpyAsync(h_flags, flags, 64, hipMemcpyDeviceToHost, c.st));
+  c.sync();
+  if (h_flags[0])
+    throw KgsError(KGS_E_NOT_WELL_CALC, gs ? "The grand-sum polynomial S is not well calculated"
+                                             : "The grand-product polynomial Z is not well calculated");
+  const int iS = ci;
+  commit_finish(c, cS, com[ci++].data());
+  lap(1);
+
+  // ---------------- round 3: quotient on a coset (prover.js:233-286)
+  tr.add_scalar(gamma);
+  tr.add_commitment(com[iS].data());
+  const Fr alpha = tr.challenge();
+  const int lcs = (!gs && !sel) ? nbits : nbits + 1;
+  const uint64_t cs = 1ull << lcs;
+  const uint32_t rot = (uint32_t)(cs >> nbits);
+  const uint64_t qlen = (!gs && !sel) ? n - 1 : 2 * n - 2;  // deg Q + 1 bound
+  Fr gn = Fr::from_u64(5).pow_u64(n);
+  Fr qs[4] = {alpha, gamma, (gn - Fr::one()).inverse(), (gn.neg() - Fr::one()).inverse()};
+  uint32_t* d_qs = c.scal(qs, 4);
+  launch_divcheck(c.st, !gs, sel, flags + 1, Sev, fcomb, tcomb, in.sel_f, in.sel_t, d_qs, n);
+  uint32_t* cosS = c.buf("cosS", 32 * cs);
+  uint32_t* cosF = c.buf("cosF", 32 * cs);
+  uint32_t* cosT = c.buf("cosT", 32 * cs);
+  uint32_t *cosSF = nullptr, *cosST = nullptr;
+  coset_fwd(c, cosS, Sc, n, lcs);
+  coset_fwd(c, cosF, polF, n, lcs);
+  coset_fwd(c, cosT, polT, n, lcs);
+  if (sel) {
+    cosSF = c.buf("cosSF", 32 * cs);
+    cosST = c.buf("cosST", 32 * cs);
+    coset_fwd(c, cosSF, sFc, n, lcs);
+    coset_fwd(c, cosST, sTc, n, lcs);
+  }
+  uint32_t* Qc = c.buf("Qc", 32 * cs);
+  uint32_t* nxm1 = get_nxm1(c, nbits, lcs);
+  launch_quotient(c.st, !gs, sel, Qc, cosS, cosF, cosT, cosSF, cosST, nxm1, d_qs, lcs, rot);
+  coset_inv(c, Qc, Qc, lcs);
+  check_launch();
+  Commit cQ = commit_launch(c, Qc, qlen, slot++);
+  HC(hipMemcpyAsync(h_flags, flags, 64, hipMemcpyDeviceToHost, c.st));
+  c.sync();
+  if (h_flags[1]) throw KgsError(KGS_E_NOT_DIVISIBLE, "Polynomial is not divisible");
+  const int iQ = ci;
+  commit_finish(c, cQ, com[ci++].data());
+  lap(2);
+
+  // ---------------- round 4: evaluations (prover.js:288-318)
+  tr.add_scalar(alpha);
+  tr.add_commitment(com[iQ].data());
+  const Fr xi = tr.challenge();
+  const Fr w = fr_w(nbits);
+  const Fr xiw = xi * w;
+  std::vector<const uint32_t*> esrc;
+  std::vector<uint64_t> elen;
+  for (int i = 0; i < k; i++) {
+    esrc.push_back(Fc[i]);
+    elen.push_back(n);
+    if (gs) {
+      esrc.push_back(Tc[i]);
+      elen.push_back(n);
+    }
+  }
+  if (sel) {
+    esrc.push_back(sFc);
+    elen.push_back(n);
+    esrc.push_back(sTc);
+    elen.push_back(n);
+  }
+  EvalJob ej1 = eval_launch(c, esrc, elen, xi, 0);
+  EvalJob ej2 = eval_launch(c, {Sc}, {n}, xiw, 1);
+  c.sync();
+  std::vector<Fr> ev1 = eval_finish(ej1);
+  const Fr sxiw = eval_finish(ej2)[0];
+  std::vector<Fr> fx(k), tx(k);
+  size_t p = 0;
+  for (int i = 0; i < k; i++) {
+    fx[i] = ev1[p++];
+    if (gs) tx[i] = ev1[p++];
+  }
+  Fr sFx = Fr::zero(), sTx = Fr::zero();
+  if (sel) {
+    sFx = ev1[p++];
+    sTx = ev1[p++];
+  }
+  std::vector<Fr> evals;  // proof order
+  for (int i = 0; i < k; i++) {
+    evals.push_back(fx[i]);
+    if (gs) evals.push_back(tx[i]);
+  }
+  if (sel) {
+    evals.push_back(sFx);
+    evals.push_back(sTx);
+  }
+  evals.push_back(sxiw);
+  lap(3);
+
+  // ---------------- round 5: linearisation + openings (prover.js:320-413)
+  tr.add_scalar(xi);
+  for (int i = 0; i < k; i++) {
+    tr.add_scalar(fx[i]);
+    if (gs) tr.add_scalar(tx[i]);
+  }
+  if (sel) {
+    tr.add_scalar(sFx);
+    tr.add_scalar(sTx);
+  }
+  tr.add_scalar(sxiw);
+  const Fr v = tr.challenge();
+  // Z_H(xi), L1(xi) (polynomial_utils.js)
+  Fr xn = xi;
+  for (int i = 0; i < nbits; i++) xn = xn.sqr();
+  const Fr zh = xn - Fr::one();
+  const Fr l1 = zh * (Fr::from_u64(n) * (xi - Fr::one())).inverse();
+  Fr fxi = Fr::zero(), txi = Fr::zero();
+  for (int i = k - 1; i >= 0; i--) {
+    fxi = fxi * beta + fx[i];
+    if (gs) txi = txi * beta + tx[i];
+  }
+  const Fr one = Fr::one();
+  Fr selBin = Fr::zero();  // alpha^3 selTBin + alpha^2 selFBin
+  if (sel) selBin = ((sTx - sTx.sqr()) * alpha + (sFx - sFx.sqr())) * alpha * alpha;
+  LinComb lw{};
+  Fr c0;
+  uint32_t* Pbuf;
+  uint64_t L;
+  std::vector<Fr> vp(2 * k + 4);
+  vp[0] = one;
+  for (size_t i = 1; i < vp.size(); i++) vp[i] = vp[i - 1] * v;
+  if (gs) {
+    const Fr fg = fxi + gamma, tg = txi + gamma;
+    Fr rc = sxiw * fg * tg + (sel ? sTx * fg - sFx * tg : fxi - txi);
+    c0 = selBin + alpha * rc;
+    set_lc_term(lw, Sc, n, l1 - alpha * fg * tg);
+    set_lc_term(lw, Qc, qlen, zh.neg());
+    for (int i = 0; i < k; i++) {
+      set_lc_term(lw, Fc[i], n, vp[1 + i]);
+      c0 = c0 - vp[1 + i] * fx[i];
+    }
+    for (int i = 0; i < k; i++) {
+      set_lc_term(lw, Tc[i], n, vp[1 + k + i]);
+      c0 = c0 - vp[1 + k + i] * tx[i];
+    }
+    if (sel) {
+      set_lc_term(lw, sFc, n, vp[2 * k + 1]);
+      set_lc_term(lw, sTc, n, vp[2 * k + 2]);
+      c0 = c0 - vp[2 * k + 1] * sFx - vp[2 * k + 2] * sTx;
+    }
+  } else {
+    const Fr fg = fxi + gamma;
+    const Fr dF = sel ? sFx * (fg - one) + one : fg;
+    c0 = selBin + alpha * sxiw * (sel ? sTx * (gamma - one) + one : gamma) - l1;
+    set_lc_term(lw, polT, n, alpha * sxiw * (sel ? sTx : one));
+    set_lc_term(lw, Sc, n, l1 - alpha * dF);
+    set_lc_term(lw, Qc, qlen, zh.neg());
+    for (int i = 0; i < k; i++) {
+      set_lc_term(lw, Fc[i], n, vp[1 + i]);
+      c0 = c0 - vp[1 + i] * fx[i];
+    }
+    if (sel) {
+      set_lc_term(lw, sFc, n, vp[k + 1]);
+      set_lc_term(lw, sTc, n, vp[k + 2]);
+      c0 = c0 - vp[k + 1] * sFx - vp[k + 2] * sTx;
+    }
+  }
+  c0.to_bytes((uint8_t*)lw.c0);
+  L = qlen > n ? qlen : n;
+  Pbuf = c.buf("Pw", 32 * L);
+  uint32_t* Wx = c.buf("Wxi", 32 * L);
+  launch_lincomb(c.st, Pbuf, L, lw);
+  const uint32_t dtiles = (uint32_t)((L + EVAL_TILE - 1) / EVAL_TILE);
+  launch_divide(c.st, Wx, flags + 2, Pbuf, L, xpowers(c, xi), c.buf("div_part", 32 * (dtiles + 1)),
+                c.buf("div_carry", 32 * (dtiles + 1)));
+  // W_{xi w} = (S - S(xi w)) / (X - xi w)
+  LinComb l2{};
+  set_lc_term(l2, Sc, n, one);
+  sxiw.neg().to_bytes((uint8_t*)l2.c0);
+  uint32_t* P2 = c.buf("Pw2", E);
+  uint32_t* Wxw = c.buf("Wxiw", E);
+  launch_lincomb(c.st, P2, n, l2);
+  launch_divide(c.st, Wxw, flags + 3, P2, n, xpowers(c, xiw), c.buf("div_part2", 32 * (ntiles + 1)),
+                c.buf("div_carry2", 32 * (ntiles + 1)));
+  check_launch();
+  Commit cW1 = commit_launch(c, Wx, L - 1, slot++);
+  Commit cW2 = commit_launch(c, Wxw, n - 1, slot++);
+  HC(hipMemcpyAsync(h_flags, flags, 64, hipMemcpyDeviceToHost, c.st));
+  c.sync();
+  if (h_flags[2] || h_flags[3]) throw KgsError(KGS_E_DOES_NOT_DIVIDE, "Polynomial does not divide");
+  commit_finish(c, cW1, com[ci++].data());
+  commit_finish(c, cW2, com[ci++].data());
+  lap(4);
+
+  for (int i = 0; i < ncom; i++) memcpy(com_out + 64 * i, com[i].data(), 64);
+  for (size_t i = 0; i < evals.size(); i++) evals[i].to_bytes(ev_out + 32 * i);
+  c.reset_staging();
+}
+
+int fail(const KgsError& e) {
+  g_err = e.what();
+  return e.code;
+}
+
+// ------------------------------------------------------------------ ptau I/O
+struct PtauInfo {
+  int power = 0, ceremony = 0;
+  uint64_t s2_pos = 0, s2_size = 0, s3_pos = 0, s3_size = 0;
+};
+
+PtauInfo read_ptau_header(FILE* f, const char* path) {
+  PtauInfo info;
+  char magic[4];
+  uint32_t ver, nsec;
+  if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "ptau", 4) != 0)
+    throw KgsError(KGS_E_IO, std::string(path) + ": Invalid File format");
+  if (fread(&ver, 4, 1, f) != 1 || fread(&nsec, 4, 1, f) != 1) throw KgsError(KGS_E_IO, "truncated ptau");
+  if (ver > 1) throw KgsError(KGS_E_IO, std::string(path) + ": Invalid Version");
+  uint64_t pos = 12;
+  int nheaders = 0;
+  uint64_t s1_pos = 0, s1_size = 0;
+  for (uint32_t s = 0; s < nsec; s++) {
+    uint32_t id;
+    uint64_t size;
+    if (fseeko(f, (off_t)pos, SEEK_SET) || fread(&id, 4, 1, f) != 1 || fread(&size, 8, 1, f) != 1)
+      throw KgsError(KGS_E_IO, "truncated ptau section table");
+    pos += 12;
+    if (id == 1) {
+      nheaders++;
+      s1_pos = pos;
+      s1_size = size;
+    } else if (id == 2 && !info.s2_size) {
+      info.s2_pos = pos;
+      info.s2_size = size;
+    } else if (id == 3 && !info.s3_size) {
+      info.s3_pos = pos;
+      info.s3_size = size;
+    }
+    pos += size;
+  }
+  if (!nheaders) throw KgsError(KGS_E_IO, std::string(path) + ": File has no  header");
+  if (nheaders > 1) throw KgsError(KGS_E_IO, std::string(path) + ": File has more than one header");
+  uint32_t n8;
+  uint8_t q[32];
+  uint32_t pw[2];
+  if (fseeko(f, (off_t)s1_pos, SEEK_SET) || fread(&n8, 4, 1, f) != 1 || n8 != 32 || fread(q, 1, 32, f) != 32 ||
+      fread(pw, 4, 2, f) != 2)
+    throw KgsError(KGS_E_IO, std::string(path) + ": Invalid size");
+  if (memcmp(q, host::FQ_MOD.p, 32) != 0) throw KgsError(KGS_E_IO, "ptau curve is not bn128");
+  if (4 + 32 + 8 != s1_size) throw KgsError(KGS_E_IO, "Invalid PTau header size");
+  info.power = (int)pw[0];
+  info.ceremony = (int)pw[1];
+  return info;
+}
+
+// ------------------------------------------------------------------ host G2 (synthetic ptau)
+struct Fq2 {
+  Fq a, b;  // a + b u, u^2 = -1
+  Fq2 operator+(const Fq2& o) const { return {a + o.a, b + o.b}; }
+  Fq2 operator-(const Fq2& o) const { return {a - o.a, b - o.b}; }
+  Fq2 operator*(const Fq2& o) const { return {a * o.a - b * o.b, a * o.b + b * o.a}; }
+  Fq2 inv() const {
+    Fq d = (a.sqr() + b.sqr()).inverse();
+    return {a * d, b.neg() * d};
+  }
+  bool is_zero() const { return a.is_zero() && b.is_zero(); }
+  bool operator==(const Fq2& o) const { return a == o.a && b == o.b; }
+};
+struct G2A {
+  Fq2 x, y;
+  bool inf;
+};
+G2A g2_add(const G2A& p, const G2A& q) {
+  if (p.inf) return q;
+  if (q.inf) return p;
+  Fq2 lam;
+  if (p.x == q.x) {
+    if ((p.y + q.y).is_zero()) return {p.x, p.y, true};
+    Fq2 x2 = p.x * p.x;
+    lam = (x2 + x2 + x2) * (p.y + p.y).inv();
+  } else {
+    lam = (q.y - p.y) * (q.x - p.x).inv();
+  }
+  G2A r;
+  r.inf = false;
+  r.x = lam * lam - p.x - q.x;
+  r.y = lam * (p.x - r.x) - p.y;
+  return r;
+}
+Fq fq_from_dec(const char* s) {
+  Fq acc = Fq::zero(), ten = Fq::from_u64(10);
+  for (; *s; s++) acc = acc * ten + Fq::from_u64((uint64_t)(*s - '0'));
+  return acc;
+}
+G2A g2_gen() {
+  G2A g;
+  g.inf = false;
+  g.x = {fq_from_dec("10857046999023057135944570762232829481370756359578518086990519993285655852781"),
+         fq_from_dec("11559732032986387107991004021392285783925812861821192530917403151452391805634")};
+  g.y = {fq_from_dec("8495653923123431417604973247489272438418190587263600148770280649306958101930"),
+         fq_from_dec("4082367875863433681332203403145435568316851327593401208105741076214120093531")};
+  return g;
+}
+void g2_lem(const G2A& p, uint8_t out[128]) {
+  if (p.inf) {
+    memset(out, 0, 128);
+    return;
+  }
+  p.x.a.to_bytes(out);
+  p.x.b.to_bytes(out + 32);
+  p.y.a.to_bytes(out + 64);
+  p.y.b.to_bytes(out + 96);
+}
+
+// fixed-base table (d * 2^(8j)) G, affine LEM, 32 x 256
+std::vector<uint8_t> g1_fixed_table() {
+  std::vector<uint8_t> tbl(32 * 256 * 64, 0);
+  uint8_t gen[64];
+  Fq::one().to_bytes(gen);
+  Fq::from_u64(2).to_bytes(gen + 32);
+  host::G1 base = host::G1::from_affine_lem(gen);
+  for (int j = 0; j < 32; j++) {
+    host::G1 acc = host::G1::inf();
+    for (int d = 1; d < 256; d++) {
+      acc = acc.add(base);
+      acc.to_affine_lem(&tbl[64 * (j * 256 + d)]);
+    }
+    for (int s = 0; s < 8; s++) base = base.dbl();
+  }
+  return tbl;
+}
+
+}  // namespace
+
+// ================================================================== C-ABI
+extern "C" {
+
+const char* kgs_last_error(void) { return g_err.c_str(); }
+const char* kgs_version(void) { return "kgs-mi355x 0.1 (gfx950)"; }
+
+int kgs_ctx_create(int device, kgs_ctx_t** out) {
+  try {
+    if (!out) throw KgsError(KGS_E_ARG, "out is NULL");
+    int ndev = 0;
+    HC(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) throw KgsError(KGS_E_ARG, "no such HIP device");
+    HC(hipSetDevice(device));
+    auto* c = new kgs_ctx();
+    c->device = device;
+    HC(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    c->d_scal = c->buf("scalars", kgs_ctx::SCAL_BYTES);
+    c->ensure_pin(8 << 20);
+    *out = c;
+    return KGS_OK;
+  } catch (const KgsError& e) {
+    return fail(e);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return KGS_E_HIP;
+  }
+}
+
+void kgs_ctx_destroy(kgs_ctx_t* ctx) { delete ctx; }
+
+#define API_BEGIN try {
+#define API_END                               \
+  }                                           \
+  catch (const KgsError& e) {                 \
+    return fail(e);                           \
+  }                                           \
+  catch (const std::exception& e) {           \
+    g_err = e.what();                         \
+    return KGS_E_HIP;                         \
+  }                                           \
+  return KGS_OK;
+
+int kgs_srs_load_points(kgs_ctx_t* ctx, const uint8_t* g1_lem, uint64_t npts, int power, int nbits_max) {
+  API_BEGIN
+  if (!ctx || !g1_lem) throw KgsError(KGS_E_ARG, "NULL argument");
+  HC(hipSetDevice(ctx->device));
+  if (nbits_max < 0) nbits_max = power;
+  uint64_t need = 1ull << (nbits_max + 1);
+  if (npts < need) need = npts;
+  load_points(*ctx, g1_lem, need, power, nbits_max, "mem");
+  API_END
+}
+
+int kgs_srs_load_ptau(kgs_ctx_t* ctx, const char* path, int nbits_max) {
+  API_BEGIN
+  if (!ctx || !path) throw KgsError(KGS_E_ARG, "NULL argument");
+  HC(hipSetDevice(ctx->device));
+  FILE* f = fopen(path, "rb");
+  if (!f) throw KgsError(KGS_E_IO, std::string("cannot open ") + path);
+  std::unique_ptr<FILE, int (*)(FILE*)> guard(f, fclose);
+  PtauInfo info = read_ptau_header(f, path);
+  if (nbits_max < 0 || nbits_max > info.power) nbits_max = info.power;
+  std::string key = std::string(path) + "#" + std::to_string(nbits_max);
+  if (ctx->srs_key == key) return KGS_OK;
+  uint64_t avail = info.s2_size / 64;
+  uint64_t need = 1ull << (nbits_max + 1);
+  if (need > avail) need = avail;
+  std::vector<uint8_t> pts(need * 64);
+  if (fseeko(f, (off_t)info.s2_pos, SEEK_SET) || fread(pts.data(), 1, pts.size(), f) != pts.size())
+    throw KgsError(KGS_E_IO, "cannot read tauG1 section");
+  load_points(*ctx, pts.data(), need, info.power, nbits_max, key);
+  API_END
+}
+
+int kgs_srs_info(kgs_ctx_t* ctx, int* power, uint64_t* npts, int* window_c) {
+  API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  if (power) *power = ctx->srs_power;
+  if (npts) *npts = ctx->tb.npts;
+  if (window_c) *window_c = ctx->tb.c;
+  API_END
+}
+
+int kgs_ptau_read_tau_g2(const char* path, uint8_t out128[128]) {
+  API_BEGIN
+  FILE* f = fopen(path, "rb");
+  if (!f) throw KgsError(KGS_E_IO, std::string("cannot open ") + path);
+  std::unique_ptr<FILE, int (*)(FILE*)> guard(f, fclose);
+  PtauInfo info = read_ptau_header(f, path);
+  if (info.s3_size < 256) throw KgsError(KGS_E_IO, "tauG2 section too small");
+  if (fseeko(f, (off_t)(info.s3_pos + 128), SEEK_SET) || fread(out128, 1, 128, f) != 128)
+    throw KgsError(KGS_E_IO, "cannot read [tau]_2");
+  API_END
+}
+
+int kgs_ptau_write_synthetic(kgs_ctx_t* ctx, const char* path, int power, const uint8_t tau_std[32]) {
+  API_BEGIN
+  if (!path || !tau_std || power < 1 || power > 28) throw KgsError(KGS_E_ARG, "bad argument");
+  uint64_t s[4];
+  memcpy(s, tau_std, 32);
+  Fr tau = Fr::from_std(s);
+  const uint64_t n1 = (1ull << (power + 1)) - 1;
+  std::vector<uint8_t> g1(n1 * 64);
+  std::vector<uint8_t> tbl = g1_fixed_table();
+  if (ctx) {
+    HC(hipSetDevice(ctx->device));
+    ctx->reset_staging();
+    uint32_t* d_tau = ctx->scal(&tau, 1);
+    uint32_t* pw = ctx->buf("syn_pow", 32 * n1);
+    uint32_t* xy = ctx->buf("syn_xyzz", 128 * n1);
+    uint32_t* scr = ctx->buf("syn_scr", 32 * n1);
+    uint32_t* aff = ctx->buf("syn_aff", 64 * n1);
+    uint32_t* dtbl = ctx->buf("syn_tbl", tbl.size());
+    HC(hipMemcpyAsync(dtbl, tbl.data(), tbl.size(), hipMemcpyHostToDevice, ctx->st));
+    launch_powers(ctx->st, pw, n1, d_tau, nullptr);
+    launch_fixed_base(ctx->st, xy, pw, n1, dtbl);
+    launch_batch_affine(ctx->st, aff, xy, scr, n1);
+    check_launch();
+    HC(hipMemcpyAsync(g1.data(), aff, g1.size(), hipMemcpyDeviceToHost, ctx->st));
+    ctx->reset_staging();
+  } else {
+    Fr t = Fr::one();
+    for (uint64_t i = 0; i < n1; i++) {
+      uint64_t e[4];
+      t.to_std(e);
+      host::G1 acc = host::G1::inf();
+      for (int j = 0; j < 32; j++) {
+        unsigned d = (unsigned)((e[j >> 3] >> (8 * (j & 7))) & 0xff);
+        if (d) acc = acc.add(host::G1::from_affine_lem(&tbl[64 * (j * 256 + d)]));
+      }
+      acc.to_affine_lem(&g1[64 * i]);
+      t = t * tau;
+    }
+  }
+  // [1]_2, [tau]_2
+  G2A g = g2_gen(), acc{g.x, g.y, true}, base = g;
+  uint64_t e[4];
+  tau.to_std(e);
+  for (int i = 0; i < 256; i++) {
+    if ((e[i >> 6] >> (i & 63)) & 1) acc = g2_add(acc, base);
+    base = g2_add(base, base);
+  }
+  uint8_t g2[256];
+  g2_lem(g, g2);
+  g2_lem(acc, g2 + 128);
+  FILE* f = fopen(path, "wb");
+  if (!f) throw KgsError(KGS_E_IO, std::string("cannot create ") + path);
+  std::unique_ptr<FILE, int (*)(FILE*)> guard(f, fclose);
+  auto w32 = [&](uint32_t x) { fwrite(&x, 4, 1, f); };
+  auto w64 = [&](uint64_t x) { fwrite(&x, 8, 1, f); };
+  fwrite("ptau", 1, 4, f);
+  w32(1);
+  w32(3);
+  w32(1);
+  w64(44);
+  w32(32);
+  fwrite(host::FQ_MOD.p, 1, 32, f);
+  w32((uint32_t)power);
+  w32((uint32_t)power);
+  w32(2);
+  w64(g1.size());
+  fwrite(g1.data(), 1, g1.size(), f);
+  w32(3);
+  w64(256);
+  if (fwrite(g2, 1, 256, f) != 256) throw KgsError(KGS_E_IO, "write failed");
+  API_END
+}
+
+int kgs_proof_shape(int kind, int npols, int selected, int* n_commitments, int* n_evaluations) {
+  if (n_commitments) *n_commitments = 2 * npols + (selected ? 2 : 0) + 4;
+  if (n_evaluations) *n_evaluations = (kind == KGS_GRANDSUM ? 2 : 1) * npols + (selected ? 2 : 0) + 1;
+  return KGS_OK;
+}
+
+int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* const* evals_f,
+              const uint8_t* const* evals_t, const uint8_t* sel_f, const uint8_t* sel_t, uint8_t* const* mont_f,
+              uint8_t* const* mont_t, uint8_t* commitments_out, uint8_t* evaluations_out) {
+  API_BEGIN
+  if (!ctx || !evals_f || !evals_t || !commitments_out || !evaluations_out) throw KgsError(KGS_E_ARG, "NULL argument");
+  if ((sel_f == nullptr) != (sel_t == nullptr)) throw KgsError(KGS_E_ARG, "selectors must be both given or both NULL");
+  if (npols < 1 || npols > 10 || nbits < 1 || nbits > 28) throw KgsError(KGS_E_ARG, "bad shape");
+  HC(hipSetDevice(ctx->device));
+  const uint64_t n = 1ull << nbits;
+  const size_t E = 32 * n;
+  ProveIn in;
+  in.kind = kind;
+  in.nbits = nbits;
+  in.npols = npols;
+  for (int i = 0; i < npols; i++) {
+    uint32_t* df = ctx->buf("in_f" + std::to_string(i), E);
+    uint32_t* dt = ctx->buf("in_t" + std::to_string(i), E);
+    HC(hipMemcpyAsync(df, evals_f[i], E, hipMemcpyHostToDevice, ctx->st));
+    HC(hipMemcpyAsync(dt, evals_t[i], E, hipMemcpyHostToDevice, ctx->st));
+    in.f_std.push_back(df);
+    in.t_std.push_back(dt);
+    in.mont_f_out.push_back(mont_f ? mont_f[i] : nullptr);
+    in.mont_t_out.push_back(mont_t ? mont_t[i] : nullptr);
+  }
+  if (sel_f) {
+    uint32_t* a = ctx->buf("in_sf", E);
+    uint32_t* b = ctx->buf("in_st", E);
+    HC(hipMemcpyAsync(a, sel_f, E, hipMemcpyHostToDevice, ctx->st));
+    HC(hipMemcpyAsync(b, sel_t, E, hipMemcpyHostToDevice, ctx->st));
+    in.sel_f = a;
+    in.sel_t = b;
+  }
+  prove_impl(*ctx, in, commitments_out, evaluations_out);
+  API_END
+}
+
+int kgs_prove_device(kgs_ctx_t* ctx, int kind, int nbits, int npols, const void* const* d_evals_f,
+                     const void* const* d_evals_t, const void* d_sel_f, const void* d_sel_t, uint8_t* commitments_out,
+                     uint8_t* evaluations_out) {
+  API_BEGIN
+  if (!ctx || !d_evals_f || !d_evals_t || !commitments_out || !evaluations_out) throw KgsError(KGS_E_ARG, "NULL argument");
+  if ((d_sel_f == nullptr) != (d_sel_t == nullptr)) throw KgsError(KGS_E_ARG, "selectors must be both given or both NULL");
+  if (npols < 1 || npols > 10 || nbits < 1 || nbits > 28) throw KgsError(KGS_E_ARG, "bad shape");
+  HC(hipSetDevice(ctx->device));
+  ProveIn in;
+  in.kind = kind;
+  in.nbits = nbits;
+  in.npols = npols;
+  for (int i = 0; i < npols; i++) {
+    in.f_std.push_back((const uint32_t*)d_evals_f[i]);
+    in.t_std.push_back((const uint32_t*)d_evals_t[i]);
+  }
+  in.sel_f = (const uint32_t*)d_sel_f;
+  in.sel_t = (const uint32_t*)d_sel_t;
+  prove_impl(*ctx, in, commitments_out, evaluations_out);
+  API_END
+}
+
+int kgs_last_timing(kgs_ctx_t* ctx, double* rounds_ms, int max_rounds) {
+  if (!ctx || !rounds_ms) return KGS_E_ARG;
+  int n = (int)ctx->timing.size() < max_rounds ? (int)ctx->timing.size() : max_rounds;
+  for (int i = 0; i < n; i++) rounds_ms[i] = ctx->timing[i];
+  return n;
+}
+
+int kgs_fr_to_mont(kgs_ctx_t* ctx, const uint8_t* in_std, uint8_t* out_mont, uint64_t n) {
+  API_BEGIN
+  HC(hipSetDevice(ctx->device));
+  uint32_t* a = ctx->buf("prim_a", 32 * n);
+  uint32_t* b = ctx->buf("prim_b", 32 * n);
+  HC(hipMemcpyAsync(a, in_std, 32 * n, hipMemcpyHostToDevice, ctx->st));
+  launch_to_mont(ctx->st, b, a, n);
+  check_launch();
+  HC(hipMemcpyAsync(out_mont, b, 32 * n, hipMemcpyDeviceToHost, ctx->st));
+  ctx->sync();
+  API_END
+}
+
+int kgs_ntt(kgs_ctx_t* ctx, const uint8_t* in_mont, uint8_t* out_mont, int logm, int inverse) {
+  API_BEGIN
+  HC(hipSetDevice(ctx->device));
+  if (logm < 0 || logm > 28) throw KgsError(KGS_E_ARG, "bad logm");
+  if (logm > ctx->logM) ensure_domain(*ctx, logm);
+  const uint64_t m = 1ull << logm;
+  uint32_t* a = ctx->buf("prim_a", 32 * m);
+  uint32_t* b = ctx->buf("prim_b", 32 * m);
+  ctx->reset_staging();
+  HC(hipMemcpyAsync(a, in_mont, 32 * m, hipMemcpyHostToDevice, ctx->st));
+  if (inverse) {
+    intt_nat(*ctx, b, a, logm);
+  } else {
+    ntt_dif(ctx->st, a, a, m, logm, nullptr, ctx->tw_fwd, ctx->logM);
+    launch_bitrev_copy(ctx->st, b, a, logm);
+  }
+  check_launch();
+  HC(hipMemcpyAsync(out_mont, b, 32 * m, hipMemcpyDeviceToHost, ctx->st));
+  ctx->sync();
+  API_END
+}
+
+int kgs_msm(kgs_ctx_t* ctx, const uint8_t* scalars_mont, uint64_t n, uint8_t out_lem[64]) {
+  API_BEGIN
+  HC(hipSetDevice(ctx->device));
+  if (n > ctx->tb.npts) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
+  ctx->reset_staging();
+  uint32_t* a = ctx->buf("prim_a", 32 * (n ? n : 1));
+  HC(hipMemcpyAsync(a, scalars_mont, 32 * n, hipMemcpyHostToDevice, ctx->st));
+  Commit cm = commit_launch(*ctx, a, n, 0);
+  ctx->sync();
+  commit_finish(*ctx, cm, out_lem);
+  ctx->reset_staging();
+  API_END
+}
+
+int kgs_grand_build(kgs_ctx_t* ctx, int kind, const uint8_t* f_mont, const uint8_t* t_mont, const uint8_t* sel_f,
+                    const uint8_t* sel_t, const uint8_t gamma_mont[32], uint64_t n, uint8_t* out_mont) {
+  API_BEGIN
+  HC(hipSetDevice(ctx->device));
+  if ((sel_f == nullptr) != (sel_t == nullptr)) throw KgsError(KGS_E_ARG, "selectors must be both given or both NULL");
+  ctx->reset_staging();
+  const size_t E = 32 * n;
+  uint32_t* f = ctx->buf("gb_f", E);
+  uint32_t* t = ctx->buf("gb_t", E);
+  uint32_t* o = ctx->buf("gb_o", E);
+  uint32_t *sf = nullptr, *st = nullptr;
+  HC(hipMemcpyAsync(f, f_mont, E, hipMemcpyHostToDevice, ctx->st));
+  HC(hipMemcpyAsync(t, t_mont, E, hipMemcpyHostToDevice, ctx->st));
+  if (sel_f) {
+    sf = ctx->buf("gb_sf", E);
+    st = ctx->buf("gb_st", E);
+    HC(hipMemcpyAsync(sf, sel_f, E, hipMemcpyHostToDevice, ctx->st));
+    HC(hipMemcpyAsync(st, sel_t, E, hipMemcpyHostToDevice, ctx->st));
+  }
+  Fr g = Fr::from_bytes(gamma_mont);
+  uint32_t* dg = ctx->scal(&g, 1);
+  uint32_t* flags = ctx->buf("flags", 64);
+  HC(hipMemsetAsync(flags, 0, 64, ctx->st));
+  const uint32_t ntiles = (uint32_t)((n + EVAL_TILE - 1) / EVAL_TILE);
+  launch_builder(ctx->st, kind == KGS_GRANDPRODUCT, sel_f != nullptr, o, f, t, sf, st, dg, n,
+                 ctx->buf("bt_tp", 32 * (ntiles + 1)), ctx->buf("bt_ti", 32 * (ntiles + 1)), flags);
+  check_launch();
+  uint32_t* hf = (uint32_t*)ctx->pin(64);
+  HC(hipMemcpyAsync(out_mont, o, E, hipMemcpyDeviceToHost, ctx->st));
+  HC(hipMemcpyAsync(hf, flags, 64, hipMemcpyDeviceToHost, ctx->st));
+  ctx->sync();
+  bool bad = hf[0] != 0;
+  ctx->reset_staging();
+  if (bad)
+    throw KgsError(KGS_E_NOT_WELL_CALC, kind == KGS_GRANDSUM ? "The grand-sum polynomial S is not well calculated"
+                                                             : "The grand-product polynomial Z is not well calculated");
+  API_END
+}
+
+int kgs_poly_eval(kgs_ctx_t* ctx, const uint8_t* coef_mont, uint64_t len, const uint8_t x_mont[32],
+                  uint8_t out_mont[32]) {
+  API_BEGIN
+  HC(hipSetDevice(ctx->device));
+  ctx->reset_staging();
+  uint32_t* a = ctx->buf("prim_a", 32 * (len ? len : 1));
+  HC(hipMemcpyAsync(a, coef_mont, 32 * len, hipMemcpyHostToDevice, ctx->st));
+  EvalJob j = eval_launch(*ctx, {a}, {len}, Fr::from_bytes(x_mont), 0);
+  ctx->sync();
+  eval_finish(j)[0].to_bytes(out_mont);
+  ctx->reset_staging();
+  API_END
+}
+
+int kgs_poly_div_x_sub(kgs_ctx_t* ctx, const uint8_t* coef_mont, uint64_t len, const uint8_t z_mont[32],
+                       uint8_t* out_mont) {
+  API_BEGIN
+  HC(hipSetDevice(ctx->device));
+  if (len < 2) throw KgsError(KGS_E_ARG, "length must be >= 2");
+  ctx->reset_staging();
+  uint32_t* a = ctx->buf("prim_a", 32 * len);
+  uint32_t* b = ctx->buf("prim_b", 32 * len);
+  uint32_t* flags = ctx->buf("flags", 64);
+  HC(hipMemsetAsync(flags, 0, 64, ctx->st));
+  HC(hipMemcpyAsync(a, coef_mont, 32 * len, hipMemcpyHostToDevice, ctx->st));
+  const uint32_t dt = (uint32_t)((len + EVAL_TILE - 1) / EVAL_TILE);
+  launch_divide(ctx->st, b, flags, a, len, xpowers(*ctx, Fr::from_bytes(z_mont)), ctx->buf("div_part", 32 * (dt + 1)),
+                ctx->buf("div_carry", 32 * (dt + 1)));
+  check_launch();
+  uint32_t* hf = (uint32_t*)ctx->pin(64);
+  HC(hipMemcpyAsync(out_mont, b, 32 * len, hipMemcpyDeviceToHost, ctx->st));
+  HC(hipMemcpyAsync(hf, flags, 64, hipMemcpyDeviceToHost, ctx->st));
+  ctx->sync();
+  bool bad = hf[0] != 0;
+  ctx->reset_staging();
+  if (bad) throw KgsError(KGS_E_DOES_NOT_DIVIDE, "Polynomial does not divide");
+  API_END
+}
+
+int kgs_keccak256(const uint8_t* data, uint64_t len, uint8_t out[32]) {
+  host::keccak256(data, (size_t)len, out);
+  return KGS_OK;
+}
+
+int kgs_bench_msm(kgs_ctx_t* ctx, const void* d_scalars_mont, uint64_t n, int reps, double* ms) {
+  API_BEGIN
+  HC(hipSetDevice(ctx->device));
+  if (n > ctx->tb.npts) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
+  uint32_t* dT = ctx->buf("msm_T", (size_t)64 * ctx->tb.c * 128);
+  msm_run(ctx->st, ctx->tb, ctx->mw, (const uint32_t*)d_scalars_mont, n, dT);  // warm
+  hipEvent_t e0, e1;
+  HC(hipEventCreate(&e0));
+  HC(hipEventCreate(&e1));
+  HC(hipEventRecord(e0, ctx->st));
+  for (int r = 0; r < reps; r++) msm_run(ctx->st, ctx->tb, ctx->mw, (const uint32_t*)d_scalars_mont, n, dT);
+  HC(hipEventRecord(e1, ctx->st));
+  HC(hipEventSynchronize(e1));
+  float f = 0;
+  HC(hipEventElapsedTime(&f, e0, e1));
+  *ms = f;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  API_END
+}
+
+int kgs_bench_ntt(kgs_ctx_t* ctx, void* d_buf, int logm, int reps, double* ms) {
+  API_BEGIN
+  HC(hipSetDevice(ctx->device));
+  if (logm > ctx->logM) ensure_domain(*ctx, logm);
+  uint32_t* a = (uint32_t*)d_buf;
+  const uint64_t m = 1ull << logm;
+  hipEvent_t e0, e1;
+  HC(hipEventCreate(&e0));
+  HC(hipEventCreate(&e1));
+  HC(hipEventRecord(e0, ctx->st));
+  for (int r = 0; r < reps; r++) {
+    ntt_dif(ctx->st, a, a, m, logm, nullptr, ctx->tw_fwd, ctx->logM);
+    ntt_dit(ctx->st, a, a, 1, logm, ctx->tw_inv, ctx->logM, nullptr, ctx->invm + 8 * logm);
+  }
+  HC(hipEventRecord(e1, ctx->st));
+  HC(hipEventSynchronize(e1));
+  float f = 0;
+  HC(hipEventElapsedTime(&f, e0, e1));
+  *ms = f;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,558 @@
+"""Grand-sum / grand-product KZG provers and verifiers for the CPU ORACLE (test infrastructure only).
+
+Op-for-op restatement (same rounds, same transcript order, same polynomial operations and buffer
+lengths) of:
+  * src/grandsum/mset_eq_kzg_prover.js:12-434 and src/grandsum/grandsum.js:6-62
+  * src/grandproduct/mset_eq_kzg_prover.js:12-414 and src/grandproduct/grandproduct.js:6-57
+  * src/grandsum/mset_eq_kzg_verifier.js:9-313, src/grandproduct/mset_eq_kzg_verifier.js:9-299
+  * src/Keccak256Transcript.js:7-53, src/polynomial/polynomial_utils.js:1-19
+
+Inputs mirror the reference call surface: F/T evaluations are 32 B-per-element LE **standard-form**
+buffers (converted to Montgomery and written back into the caller's object, prover.js:147-148);
+selector evaluations are LE **Montgomery** buffers built from Fr.one/Fr.zero. The proof is
+`{"commitments": {name: 64 B LEM affine}, "evaluations": {name: 32 B LE Montgomery}}`.
+
+Commitments: `SRS.msm` either runs the restated Pippenger over the ptau's section-2 points, or —
+for a synthetic ptau whose tau is known — the closed form (sum c_i tau^i)·G1, which is the same
+group element (used to keep the pure-Python oracle fast; tests pin the two against each other).
+"""
+from . import bn254 as bn
+from .keccak import keccak256
+from .poly import Polynomial, Evaluations, batch_inverse
+from .ptau import PTau
+
+R = bn.R
+
+
+class EvalBuffer:
+    """Mutable stand-in for the reference `Evaluations` object (`.eval` byte buffer)."""
+
+    def __init__(self, eval_bytes):
+        self.eval = bytes(eval_bytes)
+
+    def length(self):
+        return len(self.eval) // 32
+
+    def std_values(self):
+        """Interpret `.eval` as standard-form LE (the caller-side form of F/T)."""
+        b = self.eval
+        return [int.from_bytes(b[32 * i:32 * i + 32], "little") % R for i in range(self.length())]
+
+    def mont_values(self):
+        """Interpret `.eval` as LE Montgomery (selectors; F/T after the prover ran)."""
+        b = self.eval
+        return [bn.fr_from_bytes(b[32 * i:32 * i + 32]) for i in range(self.length())]
+
+
+def mont_bytes(vals):
+    return b"".join(bn.fr_to_bytes(v) for v in vals)
+
+
+def std_bytes(vals):
+    return b"".join(bn.fr_std_to_bytes(v) for v in vals)
+
+
+class SRS:
+    def __init__(self, ptau, tau=None, use_closed_form=True):
+        self.ptau = ptau if isinstance(ptau, PTau) else PTau(ptau)
+        self.tau = tau
+        self.use_closed_form = use_closed_form and tau is not None
+
+    @property
+    def power(self):
+        return self.ptau.power
+
+    def msm(self, scalars):
+        """[ffjs] G1.multiExpAffine(PTau[0..N), scalars) + toAffine (polynomial.js:1106-1115)."""
+        if self.use_closed_form:
+            acc = 0
+            for c in reversed(scalars):
+                acc = (acc * self.tau + c) % R
+            return bn.g1_mul(bn.G1_GEN, acc)
+        bases = [self.ptau.g1_point(i) for i in range(len(scalars))]
+        return bn.g1_msm_pippenger(bases, scalars)
+
+
+class Transcript:
+    """src/Keccak256Transcript.js — cumulative, never reset between challenges."""
+
+    def __init__(self):
+        self.data = []
+
+    def add_pol_commitment(self, p):
+        self.data.append(("P", p))
+
+    def add_field_element(self, v):
+        self.data.append(("S", v))
+
+    def get_challenge(self):
+        if not self.data:
+            raise ValueError("Keccak256Transcript: No data to generate a transcript")
+        buf = b"".join(bn.g1_to_rpr_uncompressed(d) if t == "P" else (d % R).to_bytes(32, "big")
+                       for t, d in self.data)
+        return int.from_bytes(keccak256(buf), "big") % R
+
+
+def zh_eval(xi, nbits):
+    """polynomial_utils.js:1-10."""
+    xn = xi
+    for _ in range(nbits):
+        xn = xn * xn % R
+    return (xn - 1) % R
+
+
+def l1_eval(xi, zh, nbits):
+    """polynomial_utils.js:12-19."""
+    n = (1 << nbits) % R
+    return zh * pow(n * (xi - 1) % R, R - 2, R) % R
+
+
+def _as_list(x):
+    return list(x) if isinstance(x, (list, tuple)) else [x]
+
+
+def _check_inputs(srs, evalsFs, evalsTs, selF, selT):
+    """mset_eq_kzg_prover.js:22-81 (same checks, same messages)."""
+    evalsFs = _as_list(evalsFs)
+    evalsTs = _as_list(evalsTs)
+    if len(evalsFs) != len(evalsTs):
+        raise ValueError("The lengths of the two vector multisets must be the same.")
+    npols = len(evalsFs)
+    if npols == 0:
+        raise ValueError("The number of multisets must be greater than 0.")
+    for i in range(npols):
+        if evalsFs[i].length() != evalsTs[i].length():
+            raise ValueError(f"The {i}-th multiset buffers must have the same length.")
+        elif evalsFs[i].length() != evalsFs[0].length():
+            raise ValueError("The multiset buffers must all have the same length.")
+    n0 = evalsFs[0].length()
+    if selF is None:
+        selF = EvalBuffer(mont_bytes([1] * n0))
+    if selT is None:
+        selT = EvalBuffer(mont_bytes([1] * n0))
+    if selF.length() != selT.length():
+        raise ValueError("The selection buffers must have the same length.")
+    elif selF.length() != n0:
+        raise ValueError("The selection buffers must have the same length as the multiset buffers.")
+    selFv = selF.mont_values()
+    selTv = selT.mont_values()
+    is_selected = not (all(v == 1 for v in selFv) and all(v == 1 for v in selTv))
+    nbits = (n0 - 1).bit_length()
+    if n0 != 1 << nbits:
+        raise ValueError("Polynomial length must be a power of two.")
+    if srs.power < nbits:
+        raise ValueError("The Powers of Tau file is not sufficiently large to commit the polynomials.")
+    return evalsFs, evalsTs, selFv, selTv, is_selected, nbits
+
+
+def _grandsum_S(evF, evT, selF, selT, gamma):
+    """grandsum.js:6-62."""
+    n = len(evF)
+    num = [0] * n
+    den = [0] * n
+    for i in range(n):
+        f = (evF[i] + gamma) % R
+        t = (evT[i] + gamma) % R
+        num[(i + 1) % n] = (t * selF[i] - f * selT[i]) % R
+        den[(i + 1) % n] = f * t % R
+    den = batch_inverse(den)
+    last = 0
+    for i in range(n):
+        j = (i + 1) % n
+        last = (num[j] * den[j] + last) % R
+        num[j] = last
+    if num[0] != 0:
+        raise ValueError("The grand-sum polynomial S is not well calculated")
+    return Polynomial.from_evaluations(num)
+
+
+def _grandproduct_Z(evF, evT, selF, selT, gamma):
+    """grandproduct.js:6-57."""
+    n = len(evF)
+    num = [1] * n
+    den = [1] * n
+    for i in range(n):
+        a = (evF[i] + gamma) % R
+        b = (evT[i] + gamma) % R
+        num[(i + 1) % n] = (selF[i] * (a - 1) + 1) % R
+        den[(i + 1) % n] = (selT[i] * (b - 1) + 1) % R
+    den = batch_inverse(den)
+    last = 1
+    for i in range(n):
+        j = (i + 1) % n
+        last = num[j] * den[j] * last % R
+        num[j] = last
+    if num[0] != 1:
+        raise ValueError("The grand-product polynomial Z is not well calculated")
+    return Polynomial.from_evaluations(num)
+
+
+def prove(kind, srs, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, trace=None):
+    """kind in {"grandsum", "grandproduct"}; returns the proof dict (byte-level ffjs encoding)."""
+    assert kind in ("grandsum", "grandproduct")
+    gs = kind == "grandsum"
+    evalsFs, evalsTs, selFv, selTv, is_selected, nbits = _check_inputs(
+        srs, evalsFs, evalsTs, evalsSelF, evalsSelT)
+    npols = len(evalsFs)
+    n = 1 << nbits
+    is_vector = npols > 1
+    proof = {"commitments": {}, "evaluations": {}}
+    ch = {}
+    tr = Transcript()
+    commit = srs.msm
+
+    def C(poly):
+        return poly.multi_exponentiation(srs)
+
+    # ---------------- round 1 (prover.js:144-179)
+    evF_list, evT_list, polFs, polTs = [], [], [], []
+    for i in range(npols):
+        fv = evalsFs[i].std_values()
+        tv = evalsTs[i].std_values()
+        evalsFs[i].eval = mont_bytes(fv)          # side effect, prover.js:147
+        evalsTs[i].eval = mont_bytes(tv)          # prover.js:148
+        evF_list.append(fv)
+        evT_list.append(tv)
+        polFs.append(Polynomial.from_evaluations(fv))
+        polTs.append(Polynomial.from_evaluations(tv))
+    com = proof["commitments"]
+    for i in range(npols):
+        nf = f"F{i}" if is_vector else "F"
+        nt = f"T{i}" if is_vector else "T"
+        com[nf] = C(polFs[i])
+        com[nt] = C(polTs[i])
+    selF = selT = None
+    if is_selected:
+        selF = Polynomial.from_evaluations(selFv)
+        selT = Polynomial.from_evaluations(selTv)
+        com["selF"] = C(selF)
+        com["selT"] = C(selT)
+
+    # ---------------- round 2 (prover.js:181-231)
+    for i in range(npols):
+        tr.add_pol_commitment(com[f"F{i}" if is_vector else "F"])
+        tr.add_pol_commitment(com[f"T{i}" if is_vector else "T"])
+    if is_selected:
+        tr.add_pol_commitment(com["selF"])
+        tr.add_pol_commitment(com["selT"])
+    if is_vector:
+        ch["beta"] = tr.get_challenge()
+        tr.add_field_element(ch["beta"])
+    ch["gamma"] = gamma = tr.get_challenge()
+    if is_vector:
+        polF = Polynomial.zero(n)
+        polT = Polynomial.zero(n)
+        for i in range(npols - 1, -1, -1):
+            polF.mul_scalar(ch["beta"]).add(polFs[i])
+            polT.mul_scalar(ch["beta"]).add(polTs[i])
+        evF = Evaluations.from_polynomial(polF, 1).vals
+        evT = Evaluations.from_polynomial(polT, 1).vals
+    else:
+        polF, polT = polFs[0], polTs[0]
+        evF, evT = evF_list[0], evT_list[0]
+    if gs:
+        polS = _grandsum_S(evF, evT, selFv, selTv, gamma)
+        zname, ename = "S", "sxiw"
+    else:
+        polS = _grandproduct_Z(evF, evT, selFv, selTv, gamma)
+        zname, ename = "Z", "zxiw"
+    com[zname] = C(polS)
+    if trace is not None:
+        trace["S_coef"] = list(polS.coef)
+
+    # ---------------- round 3 (prover.js:233-286)
+    tr.add_field_element(gamma)
+    tr.add_pol_commitment(com[zname])
+    ch["alpha"] = alpha = tr.get_challenge()
+    polQ = Polynomial.zero(n)
+    if is_selected:
+        b1 = selT.clone()
+        b1.multiply(selT.clone())
+        polQ.add(selT.clone().sub(b1)).mul_scalar(alpha)
+        b1 = selF.clone()
+        b1.multiply(selF.clone())
+        polQ.add(selF.clone().sub(b1)).mul_scalar(alpha)
+    polQ1 = polS.clone()
+    polQ1.shift_omega()
+    polFG = polF.clone().add_scalar(gamma)
+    polTG = polT.clone().add_scalar(gamma)
+    if gs:
+        polQ1.sub(polS)
+        polQ1.multiply(polFG)
+        polQ1.multiply(polTG)
+        if is_selected:
+            sfg = selF.clone()
+            sfg.multiply(polTG)
+            stg = selT.clone()
+            stg.multiply(polFG)
+            polQ1.add(stg)
+            polQ1.sub(sfg)
+        else:
+            polQ1.add(polF)
+            polQ1.sub(polT)
+        polQ.add(polQ1).mul_scalar(alpha)
+        polQ2 = polS.clone()
+        polQ2.multiply(Polynomial.lagrange1(nbits))
+        polQ.add(polQ2)
+    else:
+        polQ2 = polS.clone()
+        if is_selected:
+            polTG.sub_scalar(1)
+            polTG.multiply(selT.clone())
+            polTG.add_scalar(1)
+            polQ1.multiply(polTG)
+            polFG.sub_scalar(1)
+            polFG.multiply(selF.clone())
+            polFG.add_scalar(1)
+            polQ2.multiply(polFG)
+        else:
+            polQ1.multiply(polTG)
+            polQ2.multiply(polFG)
+        polQ1.sub(polQ2)
+        polQ.add(polQ1).mul_scalar(alpha)
+        polQ3 = polS.clone()
+        polQ3.sub_scalar(1)
+        polQ3.multiply(Polynomial.lagrange1(nbits))
+        polQ.add(polQ3)
+    polQ.div_zh(n)
+    com["Q"] = C(polQ)
+    if trace is not None:
+        trace["Q_coef"] = list(polQ.coef)
+
+    # ---------------- round 4 (prover.js:288-318)
+    tr.add_field_element(alpha)
+    tr.add_pol_commitment(com["Q"])
+    ch["xi"] = xi = tr.get_challenge()
+    ev = {}
+    for i in range(npols):
+        ev[f"f{i}xi" if is_vector else "fxi"] = polFs[i].evaluate(xi)
+        if gs:
+            ev[f"t{i}xi" if is_vector else "txi"] = polTs[i].evaluate(xi)
+    if is_selected:
+        ev["selFxi"] = selF.evaluate(xi)
+        ev["selTxi"] = selT.evaluate(xi)
+    w = bn.FR_W[nbits]
+    ev[ename] = polS.evaluate(xi * w % R)
+
+    # ---------------- round 5 (prover.js:320-413)
+    tr.add_field_element(xi)
+    for i in range(npols):
+        tr.add_field_element(ev[f"f{i}xi" if is_vector else "fxi"])
+        if gs:
+            tr.add_field_element(ev[f"t{i}xi" if is_vector else "txi"])
+    if is_selected:
+        tr.add_field_element(ev["selFxi"])
+        tr.add_field_element(ev["selTxi"])
+    tr.add_field_element(ev[ename])
+    ch["v"] = v = tr.get_challenge()
+    zh = zh_eval(xi, nbits)
+    l1 = l1_eval(xi, zh, nbits)
+    polR = Polynomial.zero(n)
+    if is_selected:
+        sT = ev["selTxi"]
+        sF = ev["selFxi"]
+        polR.add_scalar((sT - sT * sT) % R).mul_scalar(alpha)
+        polR.add_scalar((sF - sF * sF) % R).mul_scalar(alpha)
+    fxi = polF.evaluate(xi)
+    if gs:
+        polR1 = polS.clone().mul_scalar(R - 1).add_scalar(ev[ename])
+        txi = polT.evaluate(xi)
+        fg = (fxi + gamma) % R
+        tg = (txi + gamma) % R
+        polR1.mul_scalar(fg)
+        polR1.mul_scalar(tg)
+        if is_selected:
+            polR1.add_scalar(ev["selTxi"] * fg % R)
+            polR1.sub_scalar(ev["selFxi"] * tg % R)
+        else:
+            polR1.add_scalar(fxi)
+            polR1.sub_scalar(txi)
+        polR.add(polR1).mul_scalar(alpha)
+        polR.add(polS.clone().mul_scalar(l1))
+    else:
+        polR1 = Polynomial.zero(n)
+        fg = (fxi + gamma) % R
+        tgp = polT.clone().add_scalar(gamma)        # prover.js:353 mutates polT; no value effect
+        if is_selected:
+            fg = (fg - 1) % R
+            tgp.sub_scalar(1)
+            sfg = (ev["selFxi"] * fg + 1) % R
+            stg = tgp.mul_scalar(ev["selTxi"]).add_scalar(1)
+            stg.mul_scalar(ev[ename])
+            polR1.add(stg)
+            polR1.sub(polS.clone().mul_scalar(sfg))
+        else:
+            tgp.mul_scalar(ev[ename])
+            polR1.add(tgp)
+            polR1.sub(polS.clone().mul_scalar(fg))
+        polR.add(polR1).mul_scalar(alpha)
+        polR.add(polS.clone().sub_scalar(1).mul_scalar(l1))
+    polR.sub(polQ.clone().mul_scalar(zh))
+
+    polW = Polynomial.zero(n)
+    if is_selected:
+        polW.add(selT.clone().sub_scalar(ev["selTxi"]))
+        polW.mul_scalar(v).add(selF.clone().sub_scalar(ev["selFxi"]))
+    if gs:
+        for i in range(npols - 1, -1, -1):
+            polW.mul_scalar(v).add(polTs[i].clone().sub_scalar(ev[f"t{i}xi" if is_vector else "txi"]))
+    for i in range(npols - 1, -1, -1):
+        polW.mul_scalar(v).add(polFs[i].clone().sub_scalar(ev[f"f{i}xi" if is_vector else "fxi"]))
+    polW.mul_scalar(v).add(polR.clone())
+    polW.div_by_x_sub_value(xi)
+    polWw = polS.clone().sub_scalar(ev[ename])
+    polWw.div_by_x_sub_value(xi * w % R)
+    com["Wxi"] = C(polW)
+    com["Wxiw"] = C(polWw)
+    if trace is not None:
+        trace["challenges"] = dict(ch)
+
+    return {
+        "commitments": {k: bn.g1_to_lem(p) for k, p in com.items()},
+        "evaluations": {k: bn.fr_to_bytes(x) for k, x in ev.items()},
+    }
+
+
+def verify(kind, ptau, proof, nbits, tau=None):
+    """src/grandsum/mset_eq_kzg_verifier.js:9-313 / src/grandproduct/mset_eq_kzg_verifier.js:9-299.
+
+    With `tau` given, the final pairing check e(-A,[tau]_2)·e(B,[1]_2) == 1 is decided by the
+    equivalent trapdoor test tau·A == B (same verdict, much faster); otherwise the restated
+    optimal-ate pairing is used.
+    """
+    gs = kind == "grandsum"
+    zname, ename = ("S", "sxiw") if gs else ("Z", "zxiw")
+    if not isinstance(ptau, PTau):
+        ptau = PTau(ptau)
+    com = {k: bn.g1_from_lem(b) for k, b in proof["commitments"].items()}
+    evr = dict(proof["evaluations"])
+    nF = len([k for k in com if k.startswith("F") and k[1:].isdigit()])
+    npols = nF if nF > 0 else 1
+    is_vector = npols > 1
+    is_selected = "selF" in com
+    # validateCommitments / validateEvaluations (verifier.js:194-244)
+    for k, p in com.items():
+        if not bn.g1_is_on_curve(p):
+            return False
+    for k, b in evr.items():
+        if int.from_bytes(b, "little") >= R:
+            return False
+    ev = {k: bn.fr_from_bytes(b) for k, b in evr.items()}
+    nameF = (lambda i: f"F{i}") if is_vector else (lambda i: "F")
+    nameT = (lambda i: f"T{i}") if is_vector else (lambda i: "T")
+    namef = (lambda i: f"f{i}xi") if is_vector else (lambda i: "fxi")
+    namet = (lambda i: f"t{i}xi") if is_vector else (lambda i: "txi")
+    # computeChallenges (verifier.js:246-312)
+    tr = Transcript()
+    ch = {}
+    for i in range(npols):
+        tr.add_pol_commitment(com[nameF(i)])
+        tr.add_pol_commitment(com[nameT(i)])
+    if is_selected:
+        tr.add_pol_commitment(com["selF"])
+        tr.add_pol_commitment(com["selT"])
+    if is_vector:
+        ch["beta"] = tr.get_challenge()
+        tr.add_field_element(ch["beta"])
+    beta = ch.get("beta", 0)     # Appendix C.4: undefined beta multiplies zero
+    ch["gamma"] = gamma = tr.get_challenge()
+    tr.add_field_element(gamma)
+    tr.add_pol_commitment(com[zname])
+    ch["alpha"] = alpha = tr.get_challenge()
+    tr.add_field_element(alpha)
+    tr.add_pol_commitment(com["Q"])
+    ch["xi"] = xi = tr.get_challenge()
+    tr.add_field_element(xi)
+    for i in range(npols):
+        tr.add_field_element(ev[namef(i)])
+        if gs:
+            tr.add_field_element(ev[namet(i)])
+    if is_selected:
+        tr.add_field_element(ev["selFxi"])
+        tr.add_field_element(ev["selTxi"])
+    tr.add_field_element(ev[ename])
+    ch["v"] = v = tr.get_challenge()
+    tr.add_field_element(v)
+    tr.add_pol_commitment(com["Wxi"])
+    tr.add_pol_commitment(com["Wxiw"])
+    ch["u"] = u = tr.get_challenge()
+
+    zh = zh_eval(xi, nbits)
+    l1 = l1_eval(xi, zh, nbits)
+    w = bn.FR_W[nbits]
+    r0 = 0
+    if is_selected:
+        sT, sF = ev["selTxi"], ev["selFxi"]
+        r0 = (r0 + sT - sT * sT) * alpha % R
+        r0 = (r0 + sF - sF * sF) * alpha % R
+    fxi = 0
+    txi = 0
+    for i in range(npols - 1, -1, -1):
+        fxi = (fxi * beta + ev[namef(i)]) % R
+        if gs:
+            txi = (txi * beta + ev[namet(i)]) % R
+    M = bn.g1_mul
+    A = bn.g1_add
+    neg = bn.g1_neg
+    if gs:
+        fg = (fxi + gamma) % R
+        tg = (txi + gamma) % R
+        r01 = ev[ename] * fg * tg % R
+        if is_selected:
+            r01 = (r01 + ev["selTxi"] * fg - ev["selFxi"] * tg) % R
+        else:
+            r01 = (r01 + fxi - txi) % R
+        r0 = (r0 + r01) * alpha % R
+        d11 = ((l1 - alpha * fg * tg) + u) % R
+        D1 = A(M(com[zname], d11), neg(M(com["Q"], zh)))
+    else:
+        r01 = ev[ename]
+        if is_selected:
+            r01 = r01 * ((gamma - 1) * ev["selTxi"] + 1) % R
+        else:
+            r01 = r01 * gamma % R
+        r0 = (r0 + r01) * alpha % R
+        r0 = (r0 - l1) % R
+        fg = (fxi + gamma) % R
+        if is_selected:
+            fg = ((fg - 1) * ev["selFxi"] + 1) % R
+        d11 = ((l1 - alpha * fg) + u) % R
+        D11 = M(com[zname], d11)
+        D12 = None
+        for i in range(npols - 1, -1, -1):
+            D12 = A(M(D12, beta) if D12 is not None else None, com[nameT(i)])
+        if is_selected:
+            D12 = M(D12, ev["selTxi"])
+        D12 = M(D12, ev[ename])
+        D12 = M(D12, alpha)
+        D1 = A(A(D11, D12), neg(M(com["Q"], zh)))
+    F1 = None
+    if is_selected:
+        F1 = A(F1, com["selT"])
+        F1 = A(M(F1, v), com["selF"])
+    if gs:
+        for i in range(npols - 1, -1, -1):
+            F1 = A(M(F1, v) if F1 is not None else None, com[nameT(i)])
+    for i in range(npols - 1, -1, -1):
+        F1 = A(M(F1, v) if F1 is not None else None, com[nameF(i)])
+    F1 = A(M(F1, v) if F1 is not None else None, D1)
+    E1 = 0
+    if is_selected:
+        E1 = (E1 + ev["selTxi"]) % R
+        E1 = (E1 * v + ev["selFxi"]) % R
+    if gs:
+        for i in range(npols - 1, -1, -1):
+            E1 = (E1 * v + ev[namet(i)]) % R
+    for i in range(npols - 1, -1, -1):
+        E1 = (E1 * v + ev[namef(i)]) % R
+    E1 = (E1 * v + u * ev[ename] - r0) % R
+    E1p = M(bn.G1_GEN, E1)
+    Ap = A(com["Wxi"], M(com["Wxiw"], u))
+    if gs:
+        Bp = M(A(com["Wxi"], M(com["Wxiw"], u * w % R)), xi)
+    else:
+        Bp = A(M(com["Wxi"], xi), M(com["Wxiw"], u * xi % R * w % R))
+    Bp = A(A(Bp, F1), neg(E1p))
+    if tau is not None:
+        return M(Ap, tau) == Bp
+    return bn.pairing_eq(neg(Ap), ptau.tau_g2(), Bp, bn.G2_GEN)
