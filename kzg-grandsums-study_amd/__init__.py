@@ -73,6 +73,8 @@ def lib():
         L.kgs_keccak256.argtypes = [c_u8p, ctypes.c_uint64, c_u8p]
         L.kgs_bench_msm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_double)]
+        L.kgs_bench_msm_phases.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
         L.kgs_bench_ntt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_double)]
         _lib = L

@@ -68,7 +68,8 @@ constexpr uint64_t EVAL_TILE = 2048;
 // msm.hip
 void msm_build_table(hipStream_t st, uint32_t* table, uint64_t npts, int c, int W, uint32_t* tmp_xyzz,
                      uint32_t* scratch);
-void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* scalars, uint64_t N, uint32_t* T_out);
+void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* scalars, uint64_t N, uint32_t* T_out,
+             hipEvent_t* ev = nullptr);
 void launch_fixed_base(hipStream_t st, uint32_t* out_xyzz, const uint32_t* sc, uint64_t count, const uint32_t* tbl);
 void launch_batch_affine(hipStream_t st, uint32_t* out_aff, const uint32_t* in_xyzz, uint32_t* scratch, uint64_t npts);
 

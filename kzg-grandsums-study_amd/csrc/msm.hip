@@ -245,7 +245,10 @@ __global__ void __launch_bounds__(256) k_bitsum2(uint32_t* __restrict__ T, const
 
 // ------------------------------------------------------------------ driver (device part)
 void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* scalars, uint64_t N,
-             uint32_t* T_out) {
+             uint32_t* T_out, hipEvent_t* ev) {
+  // ev (optional, 6 events): [0] start, [1] after digits+sort, [2] after accumulate,
+  // [3] after combine, [4] after bit-sum reduction
+  if (ev) hipEventRecord(ev[0], st);
   const int c = tb.c, W = tb.W;
   const uint32_t B = 1u << (c - 1);
   const uint64_t E = N * (uint64_t)W;
@@ -254,17 +257,21 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   hipLaunchKernelGGL(k_hist, dim3(nb(E)), dim3(256), 0, st, w.counts, w.digit, E);
   hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, st, w.offsets, w.cursor, w.counts, B + 1);
   hipLaunchKernelGGL(k_scatter, dim3(nb(E)), dim3(256), 0, st, w.sorted, w.cursor, w.digit, E, N, tb.npts);
+  if (ev) hipEventRecord(ev[1], st);
   uint64_t L = E >> 18;
   if (L < 4) L = 4;
   if (L > 64) L = 64;
   const uint64_t nseg = (E + L - 1) / L;
   hipLaunchKernelGGL(k_accumulate, dim3(nb(nseg)), dim3(256), 0, st, w.bstart, w.segpart, w.sorted, w.offsets,
                      B + 1, tb.table, (uint32_t)L);
+  if (ev) hipEventRecord(ev[2], st);
   hipLaunchKernelGGL(k_combine, dim3(nb(B)), dim3(256), 0, st, w.buckets, w.bstart, w.segpart, w.offsets, B,
                      (uint32_t)L);
+  if (ev) hipEventRecord(ev[3], st);
   const uint32_t chunks = (B / 2 + 255) / 256 > 0 ? (B / 2 + 255) / 256 : 1;
   hipLaunchKernelGGL(k_bitsum1, dim3(chunks, c), dim3(256), 0, st, w.part, w.buckets, c, chunks);
   hipLaunchKernelGGL(k_bitsum2, dim3(c), dim3(256), 0, st, T_out, w.part, chunks);
+  if (ev) hipEventRecord(ev[4], st);
 }
 
 // ------------------------------------------------------------------ fixed-base (synthetic SRS)

@@ -1235,6 +1235,32 @@ int kgs_bench_msm(kgs_ctx_t* ctx, const void* d_scalars_mont, uint64_t n, int re
   API_END
 }
 
+int kgs_bench_msm_phases(kgs_ctx_t* ctx, const void* d_scalars_mont, uint64_t n, int reps, double* phase_ms,
+                         uint64_t* entries) {
+  API_BEGIN
+  HC(hipSetDevice(ctx->device));
+  if (n > ctx->tb.npts) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
+  uint32_t* dT = ctx->buf("msm_T", (size_t)64 * ctx->tb.c * 128);
+  hipEvent_t ev[5];
+  for (auto& e : ev) HC(hipEventCreate(&e));
+  for (int i = 0; i < 4; i++) phase_ms[i] = 0;
+  for (int r = 0; r < reps; r++) {
+    msm_run(ctx->st, ctx->tb, ctx->mw, (const uint32_t*)d_scalars_mont, n, dT, ev);
+    HC(hipEventSynchronize(ev[4]));
+    for (int i = 0; i < 4; i++) {
+      float f = 0;
+      HC(hipEventElapsedTime(&f, ev[i], ev[i + 1]));
+      phase_ms[i] += f;
+    }
+  }
+  const uint32_t B = 1u << (ctx->tb.c - 1);
+  uint32_t tot = 0;
+  HC(hipMemcpy(&tot, ctx->mw.offsets + (B + 1), 4, hipMemcpyDeviceToHost));
+  if (entries) *entries = tot;
+  for (auto& e : ev) hipEventDestroy(e);
+  API_END
+}
+
 int kgs_bench_ntt(kgs_ctx_t* ctx, void* d_buf, int logm, int reps, double* ms) {
   API_BEGIN
   HC(hipSetDevice(ctx->device));

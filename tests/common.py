@@ -1,0 +1,87 @@
+"""Shared helpers for the test-suite: package loader, deterministic inputs, ptau fixtures.
+
+Inputs reproduce the reference tests' patterns (test/mset_eq_kzg_grandsum.test.js:24-104):
+F random, T = F rotated by one (T[0] = F[n-1], T[i] = F[i-1]); selectors all ones except
+selF[n-1] = 0 and selT[0] = 0. Unlike the reference (unseeded Fr.random()), they are seeded.
+"""
+import hashlib
+import importlib.util
+import os
+import random
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from oracle import bn254 as bn  # noqa: E402
+from oracle import ptau as opt  # noqa: E402
+
+R = bn.R
+_PKG = None
+
+
+def load_pkg():
+    global _PKG
+    if _PKG is None:
+        spec = importlib.util.spec_from_file_location(
+            "kgs_amd", os.path.join(ROOT, "kzg-grandsums-study_amd", "__init__.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _PKG = mod
+    return _PKG
+
+
+def std_bytes(vals):
+    return b"".join(bn.fr_std_to_bytes(v) for v in vals)
+
+
+def mont_bytes(vals):
+    return b"".join(bn.fr_to_bytes(v) for v in vals)
+
+
+def make_inputs(seed, nbits, npols, selected):
+    """-> (list of F std-bytes, list of T std-bytes, selF mont-bytes|None, selT mont-bytes|None)"""
+    rnd = random.Random(seed)
+    n = 1 << nbits
+    Fs, Ts = [], []
+    for _ in range(npols):
+        f = [rnd.randrange(R) for _ in range(n)]
+        t = [f[-1]] + f[:-1]
+        Fs.append(std_bytes(f))
+        Ts.append(std_bytes(t))
+    sF = sT = None
+    if selected:
+        a = [1] * n
+        a[-1] = 0
+        b = [1] * n
+        b[0] = 0
+        sF, sT = mont_bytes(a), mont_bytes(b)
+    return Fs, Ts, sF, sT
+
+
+def inputs_digest(Fs, Ts, sF, sT):
+    h = hashlib.sha256()
+    for x in Fs + Ts + [sF or b"", sT or b""]:
+        h.update(x)
+    return h.hexdigest()
+
+
+TAU = None
+
+
+def tau():
+    global TAU
+    if TAU is None:
+        TAU = opt.bench_tau()
+    return TAU
+
+
+def oracle_ptau(power):
+    """Synthetic ptau written by the ORACLE's writer (cached under /tmp)."""
+    path = f"/tmp/kgs_test_oracle_p{power}.ptau"
+    if not os.path.exists(path):
+        tmp = path + f".{os.getpid()}"
+        opt.write_synthetic_ptau(tmp, power, tau())
+        os.replace(tmp, path)
+    return path

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/golden.json with the CPU ORACLE (Python restatement of the reference).
+
+For every case: inputs are regenerated from `seed` by tests/common.make_inputs (their sha256 is
+stored to pin the generator), the proof is produced by oracle.protocol.prove on the synthetic
+power-11 ptau (tau = keccak256("kgs-bench-tau") mod r), and checked with the oracle verifier
+(restated optimal-ate pairing) before it is written. The reference itself (JS + ffjavascript) is
+not runnable offline, so these vectors are oracle outputs: "parity pinned" by
+KATs + pairing verification, not by reference-run outputs.
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import common  # noqa: E402
+from oracle import protocol as P  # noqa: E402
+
+CASES = []
+seed = 1000
+for kind in ("grandsum", "grandproduct"):
+    for npols, selected in ((1, False), (3, False), (1, True), (3, True)):
+        for nbits in (1, 2, 3, 5, 8, 11):
+            CASES.append(dict(kind=kind, nbits=nbits, npols=npols, selected=selected, seed=seed))
+            seed += 1
+
+
+def run_case(c, srs, pairing=False):
+    Fs, Ts, sF, sT = common.make_inputs(c["seed"], c["nbits"], c["npols"], c["selected"])
+    eF = [P.EvalBuffer(x) for x in Fs]
+    eT = [P.EvalBuffer(x) for x in Ts]
+    trace = {}
+    proof = P.prove(c["kind"], srs, eF if c["npols"] > 1 else eF[0], eT if c["npols"] > 1 else eT[0],
+                    P.EvalBuffer(sF) if sF else None, P.EvalBuffer(sT) if sT else None, trace=trace)
+    return Fs, Ts, sF, sT, proof, trace
+
+
+def main():
+    path = common.oracle_ptau(11)
+    srs = P.SRS(path, common.tau())
+    out = {"ptau": {"power": 11, "tau": str(common.tau()), "writer": "oracle.ptau.write_synthetic_ptau"},
+           "cases": []}
+    for c in CASES:
+        Fs, Ts, sF, sT, proof, trace = run_case(c, srs)
+        use_pairing = c["nbits"] <= 2
+        ok = P.verify(c["kind"], srs.ptau, proof, c["nbits"], tau=None if use_pairing else common.tau())
+        assert ok, c
+        rec = dict(c)
+        rec["inputs_sha256"] = common.inputs_digest(Fs, Ts, sF, sT)
+        rec["challenges"] = {k: str(v) for k, v in trace["challenges"].items()}
+        rec["proof"] = {sec: {k: v.hex() for k, v in proof[sec].items()} for sec in ("commitments", "evaluations")}
+        out["cases"].append(rec)
+        print(c, "ok")
+    with open(os.path.join(HERE, "golden.json"), "w") as fh:
+        json.dump(out, fh, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

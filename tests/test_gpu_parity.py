@@ -1,0 +1,232 @@
+"""GPU parity tests: the HIP path (through the C-ABI, lib/libkgs.so) against the CPU oracle.
+
+Bit-exact on every output (integer arithmetic). Small sizes compare byte-for-byte with the oracle
+and the committed golden vectors; large sizes (2^16 .. 2^20) use size-independent properties:
+the proof verifies (trapdoor form of the reference's pairing check, O(1) group work) and the
+transcript-independent commitments equal the closed form f(tau)·G1 computed barycentrically from
+the evaluations.
+"""
+import json
+import os
+import random
+
+import pytest
+
+import common
+from oracle import bn254 as bn
+from oracle import poly as OP
+from oracle import protocol as P
+
+pytestmark = pytest.mark.gpu
+R = bn.R
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+
+
+@pytest.fixture(scope="module")
+def K():
+    return common.load_pkg()
+
+
+@pytest.fixture(scope="module")
+def ctx9(K):
+    c = K.Context(0)
+    c.load_ptau(common.oracle_ptau(9))
+    return c
+
+
+def rv(rnd, n):
+    return [rnd.randrange(R) for _ in range(n)]
+
+
+def unmb(b):
+    return [bn.fr_from_bytes(b[32 * i:32 * i + 32]) for i in range(len(b) // 32)]
+
+
+def test_synthetic_ptau_writer_matches_oracle(K):
+    c = K.Context(0)
+    for power in (3, 9):
+        path = f"/tmp/kgs_test_gpu_p{power}.ptau"
+        c.write_synthetic_ptau(path, power, common.tau())
+        assert open(path, "rb").read() == open(common.oracle_ptau(power), "rb").read()
+    c.close()
+
+
+def test_to_mont(ctx9):
+    rnd = random.Random(1)
+    v = rv(rnd, 777)
+    assert ctx9.fr_to_mont(common.std_bytes(v)) == common.mont_bytes(v)
+
+
+@pytest.mark.parametrize("logm", list(range(0, 13)))
+def test_ntt(ctx9, logm):
+    rnd = random.Random(logm)
+    v = rv(rnd, 1 << logm)
+    assert unmb(ctx9.ntt(common.mont_bytes(v), False)) == OP.ntt(v, False)
+    assert unmb(ctx9.ntt(common.mont_bytes(v), True)) == OP.ntt(v, True)
+
+
+def test_msm(ctx9):
+    srs = P.SRS(common.oracle_ptau(9), common.tau())
+    rnd = random.Random(2)
+    for n in (1, 2, 3, 31, 256, 1000, 1023):
+        v = rv(rnd, n)
+        assert ctx9.msm(common.mont_bytes(v)) == bn.g1_to_lem(srs.msm(v)), n
+    # degenerate scalars: zeros, ones, r-1, repeated digits
+    for v in ([0] * 5, [1] * 64, [R - 1] * 9, [1 << 200] * 17, [0, 0, 7]):
+        assert ctx9.msm(common.mont_bytes(v)) == bn.g1_to_lem(srs.msm(v))
+    assert ctx9.msm(common.mont_bytes([0] * 8)) == bytes(64)  # infinity
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("sel", [False, True])
+@pytest.mark.parametrize("nbits", [1, 4, 11, 13])
+def test_grand_builder(K, kind, sel, nbits):
+    ctx = K.Context(0)
+    ctx.load_ptau(common.oracle_ptau(3))
+    rnd = random.Random(nbits * 10 + kind)
+    n = 1 << nbits
+    f = rv(rnd, n)
+    t = [f[-1]] + f[:-1]
+    g = rnd.randrange(R)
+    sF = sT = None
+    if sel:
+        sF = [1] * n
+        sF[-1] = 0
+        sT = [1] * n
+        sT[0] = 0
+    got = ctx.grand_build(kind, common.mont_bytes(f), common.mont_bytes(t), bn.fr_to_bytes(g),
+                          common.mont_bytes(sF) if sel else None, common.mont_bytes(sT) if sel else None)
+    fn = P._grandsum_S if kind == 0 else P._grandproduct_Z
+    assert unmb(got) == OP.ntt(fn(f, t, sF or [1] * n, sT or [1] * n, g).coef, False)
+    # not a multiset -> the reference's error
+    t2 = list(t)
+    t2[3 % n] = (t2[3 % n] + 1) % R
+    with pytest.raises(K.KgsError, match="not well calculated"):
+        ctx.grand_build(kind, common.mont_bytes(f), common.mont_bytes(t2), bn.fr_to_bytes(g),
+                        common.mont_bytes(sF) if sel else None, common.mont_bytes(sT) if sel else None)
+    ctx.close()
+
+
+@pytest.mark.parametrize("L", [2, 3, 8, 2047, 2048, 2049, 6000, 70000])
+def test_eval_and_division(ctx9, L):
+    rnd = random.Random(L)
+    c = rv(rnd, L)
+    x = rnd.randrange(R)
+    assert bn.fr_from_bytes(ctx9.poly_eval(common.mont_bytes(c), bn.fr_to_bytes(x))) == OP.Polynomial(c).evaluate(x)
+    c[0] = (c[0] - OP.Polynomial(c).evaluate(x)) % R
+    q = unmb(ctx9.poly_div_x_sub(common.mont_bytes(c), bn.fr_to_bytes(x)))
+    assert q == OP.Polynomial(list(c)).div_by_x_sub_value(x).coef
+    c[0] = (c[0] + 1) % R
+    K = common.load_pkg()
+    with pytest.raises(K.KgsError, match="Polynomial does not divide"):
+        ctx9.poly_div_x_sub(common.mont_bytes(c), bn.fr_to_bytes(x))
+
+
+@pytest.mark.parametrize("case", GOLD["cases"],
+                         ids=lambda c: f'{c["kind"]}-k{c["npols"]}-s{int(c["selected"])}-n{c["nbits"]}')
+def test_golden_proofs(K, case):
+    Fs, Ts, sF, sT = common.make_inputs(case["seed"], case["nbits"], case["npols"], case["selected"])
+    assert common.inputs_digest(Fs, Ts, sF, sT) == case["inputs_sha256"]
+    eF = [K.Evaluations(x) for x in Fs]
+    eT = [K.Evaluations(x) for x in Ts]
+    fn = K.grandsum_prover if case["kind"] == "grandsum" else K.grandproduct_prover
+    proof = fn(common.oracle_ptau(11), eF if case["npols"] > 1 else eF[0], eT if case["npols"] > 1 else eT[0],
+               K.Evaluations(sF) if sF else None, K.Evaluations(sT) if sT else None)
+    got = {sec: {k: v.hex() for k, v in proof[sec].items()} for sec in ("commitments", "evaluations")}
+    assert got == case["proof"]
+    # the reference writes the Montgomery form back into the caller's objects (prover.js:147-148)
+    for i in range(case["npols"]):
+        vals = [int.from_bytes(Fs[i][32 * j:32 * j + 32], "little") for j in range(1 << case["nbits"])]
+        assert eF[i].eval == common.mont_bytes(vals)
+
+
+def test_pairing_verifies_gpu_proof(K):
+    Fs, Ts, sF, sT = common.make_inputs(77, 4, 2, True)
+    for kind, fn in (("grandsum", K.grandsum_prover), ("grandproduct", K.grandproduct_prover)):
+        proof = fn(common.oracle_ptau(9), [K.Evaluations(x) for x in Fs], [K.Evaluations(x) for x in Ts],
+                   K.Evaluations(sF), K.Evaluations(sT))
+        assert P.verify(kind, common.oracle_ptau(9), proof, 4)
+
+
+def test_error_paths(K):
+    path = common.oracle_ptau(9)
+    Fs, Ts, _, _ = common.make_inputs(5, 3, 1, False)
+    Fs2, _, _, _ = common.make_inputs(6, 3, 1, False)
+    with pytest.raises(ValueError, match="The grand-sum polynomial S is not well calculated"):
+        K.grandsum_prover(path, K.Evaluations(Fs[0]), K.Evaluations(Fs2[0]))
+    with pytest.raises(ValueError, match="The grand-product polynomial Z is not well calculated"):
+        K.grandproduct_prover(path, K.Evaluations(Fs[0]), K.Evaluations(Fs2[0]))
+    sel = common.mont_bytes([2] + [1] * 7)
+    for fn in (K.grandsum_prover, K.grandproduct_prover):
+        with pytest.raises(ValueError, match="Polynomial is not divisible"):
+            fn(path, K.Evaluations(Fs[0]), K.Evaluations(Fs[0]), K.Evaluations(sel), K.Evaluations(sel))
+    with pytest.raises(ValueError, match="Polynomial length must be a power of two."):
+        K.grandsum_prover(path, K.Evaluations(Fs[0][:96]), K.Evaluations(Ts[0][:96]))
+    big, bigT, _, _ = common.make_inputs(1, 10, 1, False)
+    with pytest.raises(ValueError, match="not sufficiently large"):
+        K.grandsum_prover(path, K.Evaluations(big[0]), K.Evaluations(bigT[0]))
+
+
+def test_trivial_identity_multiset(K):
+    """F == T: S == 0 (grand-sum) / Z == 1; commitments of zero polynomials are infinity."""
+    Fs, _, _, _ = common.make_inputs(8, 3, 1, False)
+    srs = P.SRS(common.oracle_ptau(9), common.tau())
+    for kind, fn in (("grandsum", K.grandsum_prover), ("grandproduct", K.grandproduct_prover)):
+        got = fn(common.oracle_ptau(9), K.Evaluations(Fs[0]), K.Evaluations(Fs[0]))
+        exp = P.prove(kind, srs, P.EvalBuffer(Fs[0]), P.EvalBuffer(Fs[0]))
+        assert got == exp
+
+
+def _bary_eval(vals, nbits, x):
+    """p(x) from evaluations on <w_n> (barycentric), O(n) with one batch inversion."""
+    n = 1 << nbits
+    w = bn.FR_W[nbits]
+    dens, wi = [], 1
+    ws = []
+    for i in range(n):
+        ws.append(wi)
+        dens.append((x - wi) % R)
+        wi = wi * w % R
+    inv = OP.batch_inverse(dens)
+    s = 0
+    for i in range(n):
+        s = (s + vals[i] * ws[i] % R * inv[i]) % R
+    return (pow(x, n, R) - 1) * pow(n, R - 2, R) % R * s % R
+
+
+@pytest.mark.parametrize("kind,nbits,npols,sel", [("grandsum", 16, 1, False), ("grandproduct", 16, 2, True),
+                                                  ("grandsum", 20, 1, False)])
+def test_large_proof_properties(K, kind, nbits, npols, sel):
+    ctx = K.Context(0)
+    path = f"/tmp/kgs_test_gpu_p{nbits}.ptau"
+    if not os.path.exists(path):
+        ctx.write_synthetic_ptau(path, nbits, common.tau())
+    ctx.load_ptau(path, nbits)
+    rnd = random.Random(nbits)
+    n = 1 << nbits
+    Fs, Ts, fvals = [], [], []
+    for _ in range(npols):
+        f = [rnd.getrandbits(253) for _ in range(n)]
+        fvals.append(f)
+        Fs.append(common.std_bytes(f))
+        Ts.append(common.std_bytes([f[-1]] + f[:-1]))
+    sF = sT = None
+    if sel:
+        a = [1] * n
+        a[-1] = 0
+        b = [1] * n
+        b[0] = 0
+        sF, sT = common.mont_bytes(a), common.mont_bytes(b)
+    kk = K.GRANDSUM if kind == "grandsum" else K.GRANDPRODUCT
+    coms, evs, _, _ = ctx.prove(kk, nbits, Fs, Ts, sF, sT, mont_out=False)
+    cn, en = K.proof_names(kk, npols, sel)
+    proof = {"commitments": dict(zip(cn, coms)), "evaluations": dict(zip(en, evs))}
+    from oracle.ptau import PTau
+    assert P.verify(kind, PTau(path), proof, nbits, tau=common.tau())
+    # transcript-independent commitment: C(F0) == F0(tau) G1
+    ftau = _bary_eval(fvals[0], nbits, common.tau())
+    assert proof["commitments"]["F0" if npols > 1 else "F"] == bn.g1_to_lem(bn.g1_mul(bn.G1_GEN, ftau))
+    # determinism
+    coms2, evs2, _, _ = ctx.prove(kk, nbits, Fs, Ts, sF, sT, mont_out=False)
+    assert coms2 == coms and evs2 == evs
+    ctx.close()
