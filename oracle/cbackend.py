@@ -1,0 +1,97 @@
+"""ctypes wrapper of the C restatement (oracle/c/oracle.c -> oracle/build/liboracle.so).
+
+TEST INFRASTRUCTURE / CPU BASELINE ONLY: used by tests/ as a second, independent checker for
+sizes the pure-Python oracle is too slow for, and by bench.py's `cpu_baseline` leg ("port": the
+reference op list re-stated in C with OpenMP, timed on the GPU box's host cores).
+"""
+import ctypes
+import os
+import time
+
+from . import bn254 as bn
+from .ptau import read_header, read_sections
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liboracle.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            import subprocess
+            subprocess.check_call(["make", "-C", os.path.join(HERE, "c")])
+        L = ctypes.CDLL(LIB)
+        P = ctypes.POINTER(ctypes.c_char_p)
+        L.orc_prove.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_char_p, ctypes.c_char_p,
+                                ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_msm.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p]
+        L.orc_msm.restype = None
+        L.orc_keccak256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+        L.orc_keccak256.restype = None
+        _lib = L
+    return _lib
+
+
+def load_srs_bytes(ptau_path):
+    data, sections = read_sections(ptau_path)
+    _, power, _ = read_header(data, sections)
+    p2, s2 = sections[2][0]
+    return power, data[p2:p2 + s2]
+
+
+MESSAGES = {-3: None, -4: "Polynomial is not divisible", -5: "Polynomial does not divide"}
+
+
+def prove_raw(kind, nbits, Fs, Ts, sF, sT, srs_bytes, threads=0):
+    """kind 0/1; Fs/Ts lists of std bytes; sF/sT Montgomery bytes or None -> (coms, evs)."""
+    k = len(Fs)
+    sel = sF is not None
+    nc = 2 * k + (2 if sel else 0) + 4
+    ne = (2 if kind == 0 else 1) * k + (2 if sel else 0) + 1
+    com = ctypes.create_string_buffer(64 * nc)
+    ev = ctypes.create_string_buffer(32 * ne)
+    FA = (ctypes.c_char_p * k)(*Fs)
+    TA = (ctypes.c_char_p * k)(*Ts)
+    rc = lib().orc_prove(kind, nbits, k, FA, TA, sF, sT, srs_bytes, len(srs_bytes) // 64, threads, com, ev)
+    if rc == -3:
+        raise ValueError("The grand-sum polynomial S is not well calculated" if kind == 0
+                         else "The grand-product polynomial Z is not well calculated")
+    if rc:
+        raise ValueError(MESSAGES.get(rc, f"oracle error {rc}"))
+    return [com.raw[64 * i:64 * i + 64] for i in range(nc)], [ev.raw[32 * i:32 * i + 32] for i in range(ne)]
+
+
+def msm(srs_bytes, scalars_mont, threads=0):
+    out = ctypes.create_string_buffer(64)
+    lib().orc_msm(srs_bytes, scalars_mont, len(scalars_mont) // 32, threads, out)
+    return out.raw
+
+
+def cpu_baseline(nbits, kind="grandsum", threads=0, ptau=None, max_seconds=60.0):
+    """Time the C port on the bench workload (same generator as bench.py) — 1 proof (a 2nd if the
+    first took < 10 s). Returns the bench.py `cpu_baseline` object."""
+    import numpy as np
+    n = 1 << nbits
+    rng = np.random.Generator(np.random.PCG64(0x4B5A4753))
+    w = rng.integers(0, np.iinfo(np.uint64).max, size=(n, 4), dtype=np.uint64, endpoint=True)
+    w[:, 3] &= np.uint64((1 << 61) - 1)
+    f = np.ascontiguousarray(w).view(np.uint8).reshape(n, 32)
+    t = np.roll(f, 1, axis=0)
+    _, srs = load_srs_bytes(ptau)
+    kk = 0 if kind == "grandsum" else 1
+    if threads <= 0:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    times = []
+    while True:
+        t0 = time.perf_counter()
+        prove_raw(kk, nbits, [f.tobytes()], [t.tobytes()], None, None, srs, threads)
+        times.append(time.perf_counter() - t0)
+        if sum(times) > 10.0 or len(times) >= 3 or sum(times) > max_seconds:
+            break
+    per = min(times)
+    return {"value": round(1.0 / per, 5), "unit": "proofs/s", "cores": threads, "kind": "port",
+            "sample": f"{len(times)} full {kind} proof(s) at n=2^{nbits}, k=1 (oracle/c C restatement of the "
+                      f"reference op list incl. 4n multiply, OpenMP {threads} threads); best of {len(times)}: "
+                      f"{per:.2f} s/proof"}

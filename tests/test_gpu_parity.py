@@ -230,3 +230,22 @@ def test_large_proof_properties(K, kind, nbits, npols, sel):
     coms2, evs2, _, _ = ctx.prove(kk, nbits, Fs, Ts, sF, sT, mont_out=False)
     assert coms2 == coms and evs2 == evs
     ctx.close()
+
+
+@pytest.mark.parametrize("kind,nbits,npols,sel", [("grandsum", 14, 1, False), ("grandproduct", 14, 1, False),
+                                                  ("grandsum", 13, 2, True), ("grandproduct", 13, 3, True)])
+def test_mid_size_vs_c_oracle(K, kind, nbits, npols, sel):
+    """Byte-for-byte against the C restatement at sizes the Python oracle is too slow for."""
+    from oracle import cbackend as C
+    path = f"/tmp/kgs_test_gpu_p{nbits}.ptau"
+    ctx = K.Context(0)
+    if not os.path.exists(path):
+        ctx.write_synthetic_ptau(path, nbits, common.tau())
+    ctx.load_ptau(path, nbits)
+    Fs, Ts, sF, sT = common.make_inputs(nbits * 3 + npols, nbits, npols, sel)
+    kk = K.GRANDSUM if kind == "grandsum" else K.GRANDPRODUCT
+    coms, evs, _, _ = ctx.prove(kk, nbits, Fs, Ts, sF, sT, mont_out=False)
+    _, srs = C.load_srs_bytes(path)
+    ecoms, eevs = C.prove_raw(kk, nbits, Fs, Ts, sF, sT, srs, 0)
+    assert coms == ecoms and evs == eevs
+    ctx.close()
