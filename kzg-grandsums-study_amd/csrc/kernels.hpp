@@ -31,7 +31,8 @@ struct MsmTables {
 };
 
 struct MsmWork {
-  int32_t* digit = nullptr;
+  int32_t* digit = nullptr;  // reused as the partition-pass value array
+  uint8_t* lo = nullptr;
   uint32_t *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *sorted = nullptr;
   uint32_t *bstart = nullptr, *segpart = nullptr, *buckets = nullptr, *part = nullptr;
 };

@@ -73,12 +73,16 @@ void msm_build_table(hipStream_t st, uint32_t* table, uint64_t npts, int c, int 
   }
 }
 
-// ------------------------------------------------------------------ digits + counting sort
-// digit[j*N + i] = signed c-bit digit j of from_mont(scalar_i); |digit| in [0, 2^(c-1)]
-__global__ void __launch_bounds__(256) k_digits(int32_t* __restrict__ digit, const uint32_t* __restrict__ sc,
-                                                uint64_t N, int c, int W) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
+// ------------------------------------------------------------------ digits + two-pass bucket sort
+// Entry (j, i) = (window, point) with signed digit d = digit_j(from_mont(scalar_i)); key |d| in
+// [0, B], B = 2^(c-1); key 0 entries are dropped. Sort by key without global per-entry atomics:
+//  pass 1 partitions by hi = key >> LOB (NH <= 257 partitions; LDS histogram + one global
+//          reservation per (block, partition)); digits are RECOMPUTED from the scalars instead of
+//          being materialised (one Montgomery product per scalar);
+//  pass 2 sorts every partition by lo = key & (2^LOB - 1) inside one workgroup (LDS histogram,
+//          LDS cursors) and writes the bucket offsets.
+// Order inside a bucket is unspecified (point addition is commutative).
+__device__ __forceinline__ void scalar_digits(int32_t* d, const uint32_t* sc, uint64_t i, int c, int W) {
   fr s = fr::load(sc + 8 * i).from_mont();
   const int32_t half = 1 << (c - 1);
   const uint32_t mask = (1u << c) - 1;
@@ -88,61 +92,111 @@ __global__ void __launch_bounds__(256) k_digits(int32_t* __restrict__ digit, con
     const int limb = bit >> 5, off = bit & 31;
     uint64_t w = limb < 8 ? s.v[limb] : 0;
     if (limb + 1 < 8) w |= (uint64_t)s.v[limb + 1] << 32;
-    int32_t d = (int32_t)((w >> off) & mask) + (int32_t)carry;
-    if (d > half) {
-      d -= (1 << c);
+    int32_t v = (int32_t)((w >> off) & mask) + (int32_t)carry;
+    if (v > half) {
+      v -= (1 << c);
       carry = 1;
     } else {
       carry = 0;
     }
-    digit[(uint64_t)j * N + i] = d;
+    d[j] = v;
   }
 }
 
-__global__ void k_hist(uint32_t* __restrict__ counts, const int32_t* __restrict__ digit, uint64_t E) {
-  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  int32_t d = digit[e];
-  if (d) atomicAdd(&counts[d < 0 ? -d : d], 1u);
-}
+constexpr int MSM_WMAX = 43;  // windows for c >= 6
 
-// exclusive scan of counts[0..nb) into offsets[0..nb] (single block of 1024 threads)
-__global__ void __launch_bounds__(1024) k_scan_u32(uint32_t* __restrict__ offsets, uint32_t* __restrict__ cursor,
-                                                   const uint32_t* __restrict__ counts, uint32_t nbins) {
-  __shared__ uint32_t part[1024];
-  const uint32_t t = threadIdx.x;
-  const uint32_t per = (nbins + 1023) / 1024;
-  uint32_t lo = t * per, hi = lo + per < nbins ? lo + per : nbins;
-  uint32_t s = 0;
-  for (uint32_t i = lo; i < hi; i++) s += counts[i];
-  part[t] = s;
+__global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ hi_count, const uint32_t* __restrict__ sc,
+                                                   uint64_t N, int c, int W, int lob, int NH) {
+  __shared__ uint32_t h[264];
+  for (int b = threadIdx.x; b < NH; b += 256) h[b] = 0;
   __syncthreads();
-  for (uint32_t off = 1; off < 1024; off <<= 1) {
-    uint32_t v = t >= off ? part[t - off] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < N) {
+    int32_t d[MSM_WMAX];
+    scalar_digits(d, sc, i, c, W);
+    for (int j = 0; j < W; j++) {
+      if (d[j]) atomicAdd(&h[(uint32_t)(d[j] < 0 ? -d[j] : d[j]) >> lob], 1u);
+    }
   }
-  uint32_t run = t ? part[t - 1] : 0;
-  for (uint32_t i = lo; i < hi; i++) {
-    offsets[i] = run;
-    cursor[i] = run;
-    run += counts[i];
-  }
-  if (t == 1023) offsets[nbins] = part[1023];
+  __syncthreads();
+  for (int b = threadIdx.x; b < NH; b += 256)
+    if (h[b]) atomicAdd(&hi_count[b], h[b]);
 }
 
-// sorted[pos] = (j*Nsrs + i) | sign<<31
-__global__ void k_scatter(uint32_t* __restrict__ sorted, uint32_t* __restrict__ cursor,
-                          const int32_t* __restrict__ digit, uint64_t E, uint64_t N, uint64_t Nsrs) {
-  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  int32_t d = digit[e];
-  if (!d) return;
-  uint32_t k = d < 0 ? -d : d;
-  uint32_t pos = atomicAdd(&cursor[k], 1u);
-  uint64_t j = e / N, i = e - j * N;
-  sorted[pos] = (uint32_t)(j * Nsrs + i) | (d < 0 ? 0x80000000u : 0u);
+// hi_off[p] = exclusive scan, hi_cur = copy; offsets[B+1] = total (single block)
+__global__ void __launch_bounds__(256) k_sort_scan(uint32_t* __restrict__ hi_off, uint32_t* __restrict__ hi_cur,
+                                                   const uint32_t* __restrict__ hi_count, int NH,
+                                                   uint32_t* __restrict__ offsets, uint32_t B) {
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (int p = 0; p < NH; p++) {
+      hi_off[p] = run;
+      hi_cur[p] = run;
+      run += hi_count[p];
+    }
+    hi_off[NH] = run;
+    offsets[B + 1] = run;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, uint8_t* __restrict__ tlo,
+                                                   uint32_t* __restrict__ hi_cur, const uint32_t* __restrict__ sc,
+                                                   uint64_t N, uint64_t Nsrs, int c, int W, int lob, int NH) {
+  __shared__ uint32_t cnt[264];
+  __shared__ uint32_t base[264];
+  for (int b = threadIdx.x; b < NH; b += 256) cnt[b] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int32_t d[MSM_WMAX];
+  uint32_t rank[MSM_WMAX];
+  if (i < N) {
+    scalar_digits(d, sc, i, c, W);
+    for (int j = 0; j < W; j++) {
+      if (d[j]) rank[j] = atomicAdd(&cnt[(uint32_t)(d[j] < 0 ? -d[j] : d[j]) >> lob], 1u);
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < NH; b += 256) base[b] = cnt[b] ? atomicAdd(&hi_cur[b], cnt[b]) : 0;
+  __syncthreads();
+  if (i < N) {
+    const uint32_t lomask = (1u << lob) - 1;
+    for (int j = 0; j < W; j++) {
+      if (!d[j]) continue;
+      const uint32_t k = (uint32_t)(d[j] < 0 ? -d[j] : d[j]);
+      const uint32_t pos = base[k >> lob] + rank[j];
+      tval[pos] = (uint32_t)((uint64_t)j * Nsrs + i) | (d[j] < 0 ? 0x80000000u : 0u);
+      tlo[pos] = (uint8_t)(k & lomask);
+    }
+  }
+}
+
+// one workgroup per hi partition p: counting sort by lo, bucket offsets for keys (p << lob) + lo
+__global__ void __launch_bounds__(256) k_sort_lo(uint32_t* __restrict__ sorted, uint32_t* __restrict__ offsets,
+                                                 const uint32_t* __restrict__ tval, const uint8_t* __restrict__ tlo,
+                                                 const uint32_t* __restrict__ hi_off, int lob, uint32_t B) {
+  __shared__ uint32_t cnt[256];
+  __shared__ uint32_t cur[256];
+  const int p = blockIdx.x;
+  const uint32_t nlo = 1u << lob;
+  const uint32_t s0 = hi_off[p], s1 = hi_off[p + 1];
+  for (uint32_t b = threadIdx.x; b < nlo; b += 256) cnt[b] = 0;
+  __syncthreads();
+  for (uint32_t e = s0 + threadIdx.x; e < s1; e += 256) atomicAdd(&cnt[tlo[e]], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = s0;
+    for (uint32_t b = 0; b < nlo; b++) {
+      const uint32_t key = ((uint32_t)p << lob) + b;
+      cur[b] = run;
+      if (key <= B) offsets[key] = run;
+      run += cnt[b];
+    }
+  }
+  __syncthreads();
+  for (uint32_t e = s0 + threadIdx.x; e < s1; e += 256) {
+    const uint32_t pos = atomicAdd(&cur[tlo[e]], 1u);
+    sorted[pos] = tval[e];
+  }
 }
 
 // ------------------------------------------------------------------ bucket accumulation
@@ -251,13 +305,20 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   if (ev) hipEventRecord(ev[0], st);
   const int c = tb.c, W = tb.W;
   const uint32_t B = 1u << (c - 1);
-  const uint64_t E = N * (uint64_t)W;
-  hipMemsetAsync(w.counts, 0, sizeof(uint32_t) * (B + 2), st);
-  hipLaunchKernelGGL(k_digits, dim3(nb(N)), dim3(256), 0, st, w.digit, scalars, N, c, W);
-  hipLaunchKernelGGL(k_hist, dim3(nb(E)), dim3(256), 0, st, w.counts, w.digit, E);
-  hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, st, w.offsets, w.cursor, w.counts, B + 1);
-  hipLaunchKernelGGL(k_scatter, dim3(nb(E)), dim3(256), 0, st, w.sorted, w.cursor, w.digit, E, N, tb.npts);
+  const int lob = c - 1 < 7 ? c - 1 : 7;
+  const int NH = (int)(B >> lob) + 1;
+  uint32_t* hi_count = w.counts;       // NH
+  uint32_t* hi_off = w.cursor;         // NH + 1
+  uint32_t* hi_cur = w.cursor + 272;   // NH
+  hipMemsetAsync(hi_count, 0, sizeof(uint32_t) * 272, st);
+  hipLaunchKernelGGL(k_sort_hist, dim3(nb(N)), dim3(256), 0, st, hi_count, scalars, N, c, W, lob, NH);
+  hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(256), 0, st, hi_off, hi_cur, hi_count, NH, w.offsets, B);
+  hipLaunchKernelGGL(k_sort_part, dim3(nb(N)), dim3(256), 0, st, (uint32_t*)w.digit, w.lo, hi_cur, scalars, N,
+                     tb.npts, c, W, lob, NH);
+  hipLaunchKernelGGL(k_sort_lo, dim3(NH), dim3(256), 0, st, w.sorted, w.offsets, (const uint32_t*)w.digit, w.lo,
+                     hi_off, lob, B);
   if (ev) hipEventRecord(ev[1], st);
+  const uint64_t E = N * (uint64_t)W;  // upper bound of nonzero entries
   uint64_t L = E >> 18;
   if (L < 4) L = 4;
   if (L > 64) L = 64;

@@ -274,9 +274,10 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
   c.msm_nseg_max = nseg;
   c.mw.digit = (int32_t*)c.buf("msm_digit", E * 4);
   c.mw.sorted = c.buf("msm_sorted", E * 4);
-  c.mw.counts = c.buf("msm_counts", 4 * (B + 4));
+  c.mw.lo = (uint8_t*)c.buf("msm_lo", E);
+  c.mw.counts = c.buf("msm_counts", 4 * (B + 300));
   c.mw.offsets = c.buf("msm_offsets", 4 * (B + 4));
-  c.mw.cursor = c.buf("msm_cursor", 4 * (B + 4));
+  c.mw.cursor = c.buf("msm_cursor", 4 * (B + 600));
   c.mw.bstart = c.buf("msm_bstart", 128 * (size_t)(B + 2));
   c.mw.segpart = c.buf("msm_segpart", 128 * nseg);
   c.mw.buckets = c.buf("msm_buckets", 128 * (size_t)(B + 2));
