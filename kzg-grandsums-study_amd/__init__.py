@@ -19,7 +19,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libkgs.so")
+LIB_PATH = os.environ.get("KGS_LIB") or os.path.join(_HERE, "lib", "libkgs.so")
 
 GRANDSUM = 0
 GRANDPRODUCT = 1

@@ -208,7 +208,10 @@ __device__ __forceinline__ void emit_run(uint32_t* bstart, uint32_t* segpart, ui
     acc.store(segpart + 32 * seg);
 }
 
-__global__ void __launch_bounds__(256) k_accumulate(uint32_t* __restrict__ bstart, uint32_t* __restrict__ segpart,
+#ifndef KGS_ACC_WAVES
+#define KGS_ACC_WAVES 1
+#endif
+__global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __restrict__ bstart, uint32_t* __restrict__ segpart,
                                                     const uint32_t* __restrict__ sorted,
                                                     const uint32_t* __restrict__ offsets, uint32_t nbins,
                                                     const uint32_t* __restrict__ table, uint32_t L) {
