@@ -1,0 +1,259 @@
+// N-API addon (Node >= 12, N-API 8) binding the C-ABI of libkgs.so (include/kgs.h) for the
+// JavaScript drop-in modules in js/src. Heavy calls (SRS load, prove) run in napi_async_work and
+// return Promises, like the reference's async module API.
+#include <node_api.h>
+#include <stdint.h>
+#include <string.h>
+#include <string>
+#include <vector>
+
+#include "../../include/kgs.h"
+
+#define NAPI_CALL(env, call)                                        \
+  do {                                                              \
+    if ((call) != napi_ok) {                                        \
+      napi_throw_error((env), nullptr, "N-API call failed: " #call); \
+      return nullptr;                                               \
+    }                                                               \
+  } while (0)
+
+static kgs_ctx_t* get_ctx(napi_env env, napi_value v) {
+  void* p = nullptr;
+  napi_get_value_external(env, v, &p);
+  return (kgs_ctx_t*)p;
+}
+
+static std::vector<uint8_t> bytes_of(napi_env env, napi_value v) {
+  std::vector<uint8_t> out;
+  bool is_ta = false;
+  napi_is_typedarray(env, v, &is_ta);
+  if (is_ta) {
+    napi_typedarray_type t;
+    size_t len;
+    void* data;
+    napi_value ab;
+    size_t off;
+    napi_get_typedarray_info(env, v, &t, &len, &data, &ab, &off);
+    out.assign((uint8_t*)data, (uint8_t*)data + len);
+    return out;
+  }
+  bool is_buf = false;
+  napi_is_buffer(env, v, &is_buf);
+  if (is_buf) {
+    void* data;
+    size_t len;
+    napi_get_buffer_info(env, v, &data, &len);
+    out.assign((uint8_t*)data, (uint8_t*)data + len);
+  }
+  return out;
+}
+
+static napi_value make_u8(napi_env env, const uint8_t* data, size_t len) {
+  void* buf;
+  napi_value ab, ta;
+  napi_create_arraybuffer(env, len, &buf, &ab);
+  memcpy(buf, data, len);
+  napi_create_typedarray(env, napi_uint8_array, len, ab, 0, &ta);
+  return ta;
+}
+
+static void ctx_finalize(napi_env, void* data, void*) { kgs_ctx_destroy((kgs_ctx_t*)data); }
+
+// ctxCreate(device) -> External
+static napi_value CtxCreate(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  int32_t dev = 0;
+  if (argc > 0) napi_get_value_int32(env, argv[0], &dev);
+  kgs_ctx_t* ctx = nullptr;
+  if (kgs_ctx_create(dev, &ctx) != KGS_OK) {
+    napi_throw_error(env, nullptr, kgs_last_error());
+    return nullptr;
+  }
+  napi_value ext;
+  NAPI_CALL(env, napi_create_external(env, ctx, ctx_finalize, nullptr, &ext));
+  return ext;
+}
+
+// keccak256(Uint8Array) -> Uint8Array(32)
+static napi_value Keccak(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  std::vector<uint8_t> d = bytes_of(env, argv[0]);
+  uint8_t out[32];
+  kgs_keccak256(d.data(), d.size(), out);
+  return make_u8(env, out, 32);
+}
+
+// srsInfo(ctx) -> {power, npts, windowC}
+static napi_value SrsInfo(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  int power = 0, c = 0;
+  uint64_t npts = 0;
+  if (kgs_srs_info(get_ctx(env, argv[0]), &power, &npts, &c) != KGS_OK) {
+    napi_throw_error(env, nullptr, kgs_last_error());
+    return nullptr;
+  }
+  napi_value o, v;
+  napi_create_object(env, &o);
+  napi_create_int32(env, power, &v);
+  napi_set_named_property(env, o, "power", v);
+  napi_create_double(env, (double)npts, &v);
+  napi_set_named_property(env, o, "npts", v);
+  napi_create_int32(env, c, &v);
+  napi_set_named_property(env, o, "windowC", v);
+  return o;
+}
+
+// ---------------------------------------------------------------- async work
+struct Job {
+  napi_async_work work = nullptr;
+  napi_deferred deferred = nullptr;
+  kgs_ctx_t* ctx = nullptr;
+  int op = 0;  // 0 = load ptau, 1 = prove
+  int rc = 0;
+  std::string err;
+  // load
+  std::string path;
+  int nbits_max = -1;
+  // prove
+  int kind = 0, nbits = 0, npols = 0;
+  std::vector<std::vector<uint8_t>> f, t, mf, mt;
+  std::vector<uint8_t> sf, st, com, ev;
+  bool selected = false;
+};
+
+static void job_execute(napi_env, void* data) {
+  Job* j = (Job*)data;
+  if (j->op == 0) {
+    j->rc = kgs_srs_load_ptau(j->ctx, j->path.c_str(), j->nbits_max);
+  } else {
+    int nc = 0, ne = 0;
+    kgs_proof_shape(j->kind, j->npols, j->selected ? 1 : 0, &nc, &ne);
+    j->com.resize(64 * (size_t)nc);
+    j->ev.resize(32 * (size_t)ne);
+    std::vector<const uint8_t*> fp, tp;
+    std::vector<uint8_t*> mfp, mtp;
+    const size_t E = (size_t)32 << j->nbits;
+    j->mf.assign(j->npols, std::vector<uint8_t>(E));
+    j->mt.assign(j->npols, std::vector<uint8_t>(E));
+    for (int i = 0; i < j->npols; i++) {
+      fp.push_back(j->f[i].data());
+      tp.push_back(j->t[i].data());
+      mfp.push_back(j->mf[i].data());
+      mtp.push_back(j->mt[i].data());
+    }
+    j->rc = kgs_prove(j->ctx, j->kind, j->nbits, j->npols, fp.data(), tp.data(), j->selected ? j->sf.data() : nullptr,
+                      j->selected ? j->st.data() : nullptr, mfp.data(), mtp.data(), j->com.data(), j->ev.data());
+  }
+  if (j->rc != KGS_OK) j->err = kgs_last_error();
+}
+
+static void job_complete(napi_env env, napi_status, void* data) {
+  Job* j = (Job*)data;
+  if (j->rc != KGS_OK) {
+    napi_value msg, err, code;
+    napi_create_string_utf8(env, j->err.c_str(), NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, nullptr, msg, &err);
+    napi_create_int32(env, j->rc, &code);
+    napi_set_named_property(env, err, "kgsCode", code);
+    napi_reject_deferred(env, j->deferred, err);
+  } else if (j->op == 0) {
+    napi_value u;
+    napi_get_undefined(env, &u);
+    napi_resolve_deferred(env, j->deferred, u);
+  } else {
+    napi_value o, arr;
+    napi_create_object(env, &o);
+    napi_create_array(env, &arr);
+    for (size_t i = 0; i < j->com.size() / 64; i++) napi_set_element(env, arr, (uint32_t)i, make_u8(env, &j->com[64 * i], 64));
+    napi_set_named_property(env, o, "commitments", arr);
+    napi_create_array(env, &arr);
+    for (size_t i = 0; i < j->ev.size() / 32; i++) napi_set_element(env, arr, (uint32_t)i, make_u8(env, &j->ev[32 * i], 32));
+    napi_set_named_property(env, o, "evaluations", arr);
+    napi_create_array(env, &arr);
+    for (size_t i = 0; i < j->mf.size(); i++) napi_set_element(env, arr, (uint32_t)i, make_u8(env, j->mf[i].data(), j->mf[i].size()));
+    napi_set_named_property(env, o, "montF", arr);
+    napi_create_array(env, &arr);
+    for (size_t i = 0; i < j->mt.size(); i++) napi_set_element(env, arr, (uint32_t)i, make_u8(env, j->mt[i].data(), j->mt[i].size()));
+    napi_set_named_property(env, o, "montT", arr);
+    napi_resolve_deferred(env, j->deferred, o);
+  }
+  napi_delete_async_work(env, j->work);
+  delete j;
+}
+
+static napi_value queue(napi_env env, Job* j, const char* name) {
+  napi_value promise, rname;
+  NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
+  napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &rname);
+  NAPI_CALL(env, napi_create_async_work(env, nullptr, rname, job_execute, job_complete, j, &j->work));
+  NAPI_CALL(env, napi_queue_async_work(env, j->work));
+  return promise;
+}
+
+// srsLoadPtau(ctx, path, nbitsMax) -> Promise<void>
+static napi_value SrsLoad(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Job* j = new Job();
+  j->op = 0;
+  j->ctx = get_ctx(env, argv[0]);
+  size_t len;
+  napi_get_value_string_utf8(env, argv[1], nullptr, 0, &len);
+  j->path.resize(len + 1);
+  napi_get_value_string_utf8(env, argv[1], &j->path[0], len + 1, &len);
+  j->path.resize(len);
+  if (argc > 2) napi_get_value_int32(env, argv[2], &j->nbits_max);
+  return queue(env, j, "kgs_srs_load");
+}
+
+// prove(ctx, kind, nbits, [F...], [T...], selF|null, selT|null) -> Promise<{commitments, evaluations, montF, montT}>
+static napi_value Prove(napi_env env, napi_callback_info info) {
+  size_t argc = 7;
+  napi_value argv[7];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Job* j = new Job();
+  j->op = 1;
+  j->ctx = get_ctx(env, argv[0]);
+  napi_get_value_int32(env, argv[1], &j->kind);
+  napi_get_value_int32(env, argv[2], &j->nbits);
+  uint32_t nf = 0, nt = 0;
+  napi_get_array_length(env, argv[3], &nf);
+  napi_get_array_length(env, argv[4], &nt);
+  j->npols = (int)nf;
+  for (uint32_t i = 0; i < nf; i++) {
+    napi_value e;
+    napi_get_element(env, argv[3], i, &e);
+    j->f.push_back(bytes_of(env, e));
+    napi_get_element(env, argv[4], i, &e);
+    j->t.push_back(bytes_of(env, e));
+  }
+  napi_valuetype ty;
+  napi_typeof(env, argv[5], &ty);
+  if (ty != napi_null && ty != napi_undefined) {
+    j->selected = true;
+    j->sf = bytes_of(env, argv[5]);
+    j->st = bytes_of(env, argv[6]);
+  }
+  return queue(env, j, "kgs_prove");
+}
+
+static napi_value Init(napi_env env, napi_value exports) {
+  napi_property_descriptor desc[] = {
+      {"ctxCreate", nullptr, CtxCreate, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"srsLoadPtau", nullptr, SrsLoad, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"srsInfo", nullptr, SrsInfo, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"prove", nullptr, Prove, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"keccak256", nullptr, Keccak, nullptr, nullptr, nullptr, napi_default, nullptr},
+  };
+  napi_define_properties(env, exports, sizeof(desc) / sizeof(desc[0]), desc);
+  return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, Init)

@@ -1,0 +1,7 @@
+// JavaScript host of the MI355X prover: the reference's module surface.
+module.exports = {
+    getCurveFromName: require("./src/curve").getCurveFromName,
+    Evaluations: require("./src/polynomial/evaluations").Evaluations,
+    mset_eq_kzg_grandsum_prover: require("./src/grandsum/mset_eq_kzg_prover"),
+    mset_eq_kzg_grandproduct_prover: require("./src/grandproduct/mset_eq_kzg_prover"),
+};
