@@ -33,6 +33,7 @@ struct MsmTables {
 struct MsmWork {
   int32_t* digit = nullptr;  // reused as the partition-pass value array
   uint8_t* lo = nullptr;
+  uint32_t* blockhist = nullptr;  // (NH <= 264) x ceil(N/256) per-block partition counts
   uint32_t *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *sorted = nullptr;
   uint32_t *bstart = nullptr, *segpart = nullptr, *buckets = nullptr, *part = nullptr;
 };

@@ -105,8 +105,9 @@ __device__ __forceinline__ void scalar_digits(int32_t* d, const uint32_t* sc, ui
 
 constexpr int MSM_WMAX = 43;  // windows for c >= 6
 
-__global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ hi_count, const uint32_t* __restrict__ sc,
-                                                   uint64_t N, int c, int W, int lob, int NH) {
+__global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ bh, const uint32_t* __restrict__ sc,
+                                                   uint64_t N, int c, int W, int lob, int NH, uint32_t nblk) {
+  // per-block partition histogram, stored transposed: bh[p * nblk + block]
   __shared__ uint32_t h[264];
   for (int b = threadIdx.x; b < NH; b += 256) h[b] = 0;
   __syncthreads();
@@ -119,20 +120,43 @@ __global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ hi_cou
     }
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < NH; b += 256)
-    if (h[b]) atomicAdd(&hi_count[b], h[b]);
+  for (int b = threadIdx.x; b < NH; b += 256) bh[(uint64_t)b * nblk + blockIdx.x] = h[b];
 }
 
-// hi_off[p] = exclusive scan, hi_cur = copy; offsets[B+1] = total (single block)
-__global__ void __launch_bounds__(256) k_sort_scan(uint32_t* __restrict__ hi_off, uint32_t* __restrict__ hi_cur,
-                                                   const uint32_t* __restrict__ hi_count, int NH,
-                                                   uint32_t* __restrict__ offsets, uint32_t B) {
+// grid = NH workgroups: exclusive scan of one partition's per-block counts (in place) and its total
+__global__ void __launch_bounds__(256) k_sort_scan_blocks(uint32_t* __restrict__ bh, uint32_t* __restrict__ ptot,
+                                                          uint32_t nblk) {
+  __shared__ uint32_t part[256];
+  uint32_t* row = bh + (uint64_t)blockIdx.x * nblk;
+  const uint32_t per = (nblk + 255) / 256;
+  const uint32_t lo = threadIdx.x * per, hi = lo + per < nblk ? lo + per : nblk;
+  uint32_t s = 0;
+  for (uint32_t b = lo; b < hi; b++) s += row[b];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+  for (uint32_t b = lo; b < hi; b++) {
+    uint32_t v = row[b];
+    row[b] = run;
+    run += v;
+  }
+  if (threadIdx.x == 255) ptot[blockIdx.x] = part[255];
+}
+
+// hi_off[p] = exclusive scan of partition totals; offsets[B+1] = total (single thread, NH <= 257)
+__global__ void k_sort_scan(uint32_t* __restrict__ hi_off, const uint32_t* __restrict__ ptot, int NH,
+                            uint32_t* __restrict__ offsets, uint32_t B) {
   if (threadIdx.x == 0) {
     uint32_t run = 0;
     for (int p = 0; p < NH; p++) {
       hi_off[p] = run;
-      hi_cur[p] = run;
-      run += hi_count[p];
+      run += ptot[p];
     }
     hi_off[NH] = run;
     offsets[B + 1] = run;
@@ -140,38 +164,32 @@ __global__ void __launch_bounds__(256) k_sort_scan(uint32_t* __restrict__ hi_off
 }
 
 __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, uint8_t* __restrict__ tlo,
-                                                   uint32_t* __restrict__ hi_cur, const uint32_t* __restrict__ sc,
-                                                   uint64_t N, uint64_t Nsrs, int c, int W, int lob, int NH) {
+                                                   const uint32_t* __restrict__ bh, const uint32_t* __restrict__ hi_off,
+                                                   const uint32_t* __restrict__ sc, uint64_t N, uint64_t Nsrs, int c,
+                                                   int W, int lob, int NH, uint32_t nblk) {
   __shared__ uint32_t cnt[264];
   __shared__ uint32_t base[264];
-  for (int b = threadIdx.x; b < NH; b += 256) cnt[b] = 0;
-  __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int32_t d[MSM_WMAX];
-  uint32_t rank[MSM_WMAX];
-  if (i < N) {
-    scalar_digits(d, sc, i, c, W);
-    for (int j = 0; j < W; j++) {
-      if (d[j]) rank[j] = atomicAdd(&cnt[(uint32_t)(d[j] < 0 ? -d[j] : d[j]) >> lob], 1u);
-    }
+  for (int b = threadIdx.x; b < NH; b += 256) {
+    cnt[b] = 0;
+    base[b] = hi_off[b] + bh[(uint64_t)b * nblk + blockIdx.x];
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < NH; b += 256) base[b] = cnt[b] ? atomicAdd(&hi_cur[b], cnt[b]) : 0;
-  __syncthreads();
-  if (i < N) {
-    const uint32_t lomask = (1u << lob) - 1;
-    for (int j = 0; j < W; j++) {
-      if (!d[j]) continue;
-      const uint32_t k = (uint32_t)(d[j] < 0 ? -d[j] : d[j]);
-      const uint32_t pos = base[k >> lob] + rank[j];
-      tval[pos] = (uint32_t)((uint64_t)j * Nsrs + i) | (d[j] < 0 ? 0x80000000u : 0u);
-      tlo[pos] = (uint8_t)(k & lomask);
-    }
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  int32_t d[MSM_WMAX];
+  scalar_digits(d, sc, i, c, W);
+  const uint32_t lomask = (1u << lob) - 1;
+  for (int j = 0; j < W; j++) {
+    if (!d[j]) continue;
+    const uint32_t k = (uint32_t)(d[j] < 0 ? -d[j] : d[j]);
+    const uint32_t pos = base[k >> lob] + atomicAdd(&cnt[k >> lob], 1u);
+    tval[pos] = (uint32_t)((uint64_t)j * Nsrs + i) | (d[j] < 0 ? 0x80000000u : 0u);
+    tlo[pos] = (uint8_t)(k & lomask);
   }
 }
 
 // one workgroup per hi partition p: counting sort by lo, bucket offsets for keys (p << lob) + lo
-__global__ void __launch_bounds__(256) k_sort_lo(uint32_t* __restrict__ sorted, uint32_t* __restrict__ offsets,
+__global__ void __launch_bounds__(1024) k_sort_lo(uint32_t* __restrict__ sorted, uint32_t* __restrict__ offsets,
                                                  const uint32_t* __restrict__ tval, const uint8_t* __restrict__ tlo,
                                                  const uint32_t* __restrict__ hi_off, int lob, uint32_t B) {
   __shared__ uint32_t cnt[256];
@@ -179,9 +197,9 @@ __global__ void __launch_bounds__(256) k_sort_lo(uint32_t* __restrict__ sorted, 
   const int p = blockIdx.x;
   const uint32_t nlo = 1u << lob;
   const uint32_t s0 = hi_off[p], s1 = hi_off[p + 1];
-  for (uint32_t b = threadIdx.x; b < nlo; b += 256) cnt[b] = 0;
+  for (uint32_t b = threadIdx.x; b < nlo; b += blockDim.x) cnt[b] = 0;
   __syncthreads();
-  for (uint32_t e = s0 + threadIdx.x; e < s1; e += 256) atomicAdd(&cnt[tlo[e]], 1u);
+  for (uint32_t e = s0 + threadIdx.x; e < s1; e += blockDim.x) atomicAdd(&cnt[tlo[e]], 1u);
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t run = s0;
@@ -193,7 +211,7 @@ __global__ void __launch_bounds__(256) k_sort_lo(uint32_t* __restrict__ sorted, 
     }
   }
   __syncthreads();
-  for (uint32_t e = s0 + threadIdx.x; e < s1; e += 256) {
+  for (uint32_t e = s0 + threadIdx.x; e < s1; e += blockDim.x) {
     const uint32_t pos = atomicAdd(&cur[tlo[e]], 1u);
     sorted[pos] = tval[e];
   }
@@ -310,15 +328,16 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   const uint32_t B = 1u << (c - 1);
   const int lob = c - 1 < 7 ? c - 1 : 7;
   const int NH = (int)(B >> lob) + 1;
-  uint32_t* hi_count = w.counts;       // NH
+  const uint32_t nblk = (uint32_t)nb(N);
+  uint32_t* ptot = w.counts;           // NH partition totals
   uint32_t* hi_off = w.cursor;         // NH + 1
-  uint32_t* hi_cur = w.cursor + 272;   // NH
-  hipMemsetAsync(hi_count, 0, sizeof(uint32_t) * 272, st);
-  hipLaunchKernelGGL(k_sort_hist, dim3(nb(N)), dim3(256), 0, st, hi_count, scalars, N, c, W, lob, NH);
-  hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(256), 0, st, hi_off, hi_cur, hi_count, NH, w.offsets, B);
-  hipLaunchKernelGGL(k_sort_part, dim3(nb(N)), dim3(256), 0, st, (uint32_t*)w.digit, w.lo, hi_cur, scalars, N,
-                     tb.npts, c, W, lob, NH);
-  hipLaunchKernelGGL(k_sort_lo, dim3(NH), dim3(256), 0, st, w.sorted, w.offsets, (const uint32_t*)w.digit, w.lo,
+  uint32_t* bh = w.blockhist;          // NH x nblk
+  hipLaunchKernelGGL(k_sort_hist, dim3(nblk), dim3(256), 0, st, bh, scalars, N, c, W, lob, NH, nblk);
+  hipLaunchKernelGGL(k_sort_scan_blocks, dim3(NH), dim3(256), 0, st, bh, ptot, nblk);
+  hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(64), 0, st, hi_off, ptot, NH, w.offsets, B);
+  hipLaunchKernelGGL(k_sort_part, dim3(nblk), dim3(256), 0, st, (uint32_t*)w.digit, w.lo, bh, hi_off, scalars, N,
+                     tb.npts, c, W, lob, NH, nblk);
+  hipLaunchKernelGGL(k_sort_lo, dim3(NH), dim3(1024), 0, st, w.sorted, w.offsets, (const uint32_t*)w.digit, w.lo,
                      hi_off, lob, B);
   if (ev) hipEventRecord(ev[1], st);
   const uint64_t E = N * (uint64_t)W;  // upper bound of nonzero entries

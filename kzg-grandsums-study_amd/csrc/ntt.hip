@@ -9,8 +9,9 @@
 // convolution path; a natural-order input to the inverse is gathered through bit reversal inside
 // the first pass. Coset scaling / 1/m scaling are fused into the first / last pass.
 //
-// Twiddles: one resident table tw[j] = w_M^j (j < M/2) per direction for the largest domain M;
-// stage half-distance h reads tw[t << (logM - log2(2h))].
+// Twiddles: per direction one resident STAGE table tw[h + t] = w_{2h}^t (t < h, h = 1..M/2; M
+// entries for the largest domain M), so the butterflies of one stage read consecutive twiddles
+// (coalesced: consecutive lanes have consecutive t) instead of a strided walk through w_M^j.
 #include "kernels.hpp"
 
 namespace kgs {
@@ -56,7 +57,7 @@ __global__ void __launch_bounds__(256) k_ntt_dif_pass(uint32_t* __restrict__ dat
     const int s = s0 + k;
     const int logh = logm - s - 1;           // half-distance h = 2^logh = d * 2^(K-1-k)
     const int dist = 1 << (K - 1 - k);       // register distance
-    const int twshift = logM - (logh + 1);   // w_{2h}^t = tw[t << twshift]
+    const uint64_t twbase = 1ull << logh;    // stage table: w_{2h}^t = tw[h + t]
 #pragma unroll
     for (int r = 0; r < (1 << K); r++) {
       if (r & dist) continue;
@@ -64,7 +65,7 @@ __global__ void __launch_bounds__(256) k_ntt_dif_pass(uint32_t* __restrict__ dat
       fr a = x[r], b = x[r + dist];
       x[r] = a + b;
       fr diff = a - b;
-      if (t) diff = diff * fr::load(tw + 8 * (t << twshift));
+      if (t) diff = diff * fr::load(tw + 8 * (twbase + t));
       x[r + dist] = diff;
     }
   }
@@ -104,13 +105,13 @@ __global__ void __launch_bounds__(256) k_ntt_dit_pass(uint32_t* __restrict__ dat
   for (int k = 0; k < K; k++) {
     const int s = s0 + k;  // half-distance h = 2^s = d * 2^k
     const int dist = 1 << k;
-    const int twshift = logM - (s + 1);
+    const uint64_t twbase = 1ull << s;       // stage table: w_{2h}^t = tw[h + t], h = 2^s
 #pragma unroll
     for (int r = 0; r < (1 << K); r++) {
       if (r & dist) continue;
       const uint64_t t = lo + ((uint64_t)(r & (dist - 1)) << logd);
       fr a = x[r], b = x[r + dist];
-      if (t) b = b * fr::load(tw + 8 * (t << twshift));
+      if (t) b = b * fr::load(tw + 8 * (twbase + t));
       x[r] = a + b;
       x[r + dist] = a - b;
     }

@@ -184,22 +184,30 @@ namespace {
 void ensure_domain(kgs_ctx& c, int logM) {
   if (c.logM >= logM) return;
   const uint64_t M = 1ull << logM;
-  c.tw_fwd = c.buf("tw_fwd", 32 * (M / 2 ? M / 2 : 1));
-  c.tw_inv = c.buf("tw_inv", 32 * (M / 2 ? M / 2 : 1));
+  // stage twiddle tables: tw[h + t] = w_{2h}^t for h = 2^l, l < logM (entries 1..M-1)
+  c.tw_fwd = c.buf("tw_fwd", 32 * M);
+  c.tw_inv = c.buf("tw_inv", 32 * M);
   c.coset_pow = c.buf("coset_pow", 32 * M);
   c.coset_ipow = c.buf("coset_ipow", 32 * M);
   c.invm = c.buf("invm", 32 * (logM + 1));
   c.reset_staging();
-  Fr w = fr_w(logM), wi = w.inverse();
-  Fr g = Fr::from_u64(5), gi = g.inverse();
-  Fr consts[4] = {w, wi, g, gi};
-  uint32_t* d = c.scal(consts, 4);
-  if (M / 2) {
-    launch_powers(c.st, c.tw_fwd, M / 2, d, nullptr);
-    launch_powers(c.st, c.tw_inv, M / 2, d + 8, nullptr);
+  std::vector<Fr> consts;
+  for (int l = 0; l < logM; l++) {
+    Fr w = fr_w(l + 1);
+    consts.push_back(w);
+    consts.push_back(w.inverse());
   }
-  launch_powers(c.st, c.coset_pow, M, d + 16, nullptr);
-  launch_powers(c.st, c.coset_ipow, M, d + 24, nullptr);
+  Fr g = Fr::from_u64(5);
+  consts.push_back(g);
+  consts.push_back(g.inverse());
+  uint32_t* d = c.scal(consts.data(), (int)consts.size());
+  for (int l = 0; l < logM; l++) {
+    const uint64_t h = 1ull << l;
+    launch_powers(c.st, c.tw_fwd + 8 * h, h, d + 16 * l, nullptr);
+    launch_powers(c.st, c.tw_inv + 8 * h, h, d + 16 * l + 8, nullptr);
+  }
+  launch_powers(c.st, c.coset_pow, M, d + 16 * logM, nullptr);
+  launch_powers(c.st, c.coset_ipow, M, d + 16 * logM + 8, nullptr);
   std::vector<Fr> im(logM + 1);
   for (int l = 0; l <= logM; l++) im[l] = Fr::from_u64(1ull << l).inverse();
   uint8_t* h = c.pin(32 * (logM + 1));
@@ -207,7 +215,6 @@ void ensure_domain(kgs_ctx& c, int logM) {
   HC(hipMemcpyAsync(c.invm, h, 32 * (logM + 1), hipMemcpyHostToDevice, c.st));
   check_launch();
   c.reset_staging();
-  for (auto& kv : c.nxm1) (void)kv;  // tables depend only on (nbits, lcs) and M-stride: rebuild lazily
   c.nxm1.clear();
   c.logM = logM;
 }
@@ -221,7 +228,9 @@ uint32_t* get_nxm1(kgs_ctx& c, int nbits, int lcs) {
   uint32_t* tmp = c.buf("nxm1_tmp", 32 * cs);
   Fr consts[2] = {Fr::from_u64(5), Fr::from_u64(1ull << nbits)};
   uint32_t* d = c.scal(consts, 2);
-  launch_nxm1(c.st, tmp, c.tw_fwd, (1ull << c.logM) / 2, d, d + 8, lcs, (1ull << c.logM) >> lcs);
+  // w_M^j (j < M/2) is the last stage table, tw_fwd + 8 * (M/2)
+  const uint64_t halfM = (1ull << c.logM) / 2;
+  launch_nxm1(c.st, tmp, c.tw_fwd + 8 * halfM, halfM, d, d + 8, lcs, (1ull << c.logM) >> lcs);
   launch_fr_batch_inv(c.st, out, tmp, cs);
   check_launch();
   c.nxm1[key] = out;
@@ -275,6 +284,7 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
   c.mw.digit = (int32_t*)c.buf("msm_digit", E * 4);
   c.mw.sorted = c.buf("msm_sorted", E * 4);
   c.mw.lo = (uint8_t*)c.buf("msm_lo", E);
+  c.mw.blockhist = c.buf("msm_blockhist", 4 * 264 * ((npts + 255) / 256 + 1));
   c.mw.counts = c.buf("msm_counts", 4 * (B + 300));
   c.mw.offsets = c.buf("msm_offsets", 4 * (B + 4));
   c.mw.cursor = c.buf("msm_cursor", 4 * (B + 600));
