@@ -59,9 +59,10 @@ __global__ void __launch_bounds__(256) k_ntt_dif_pass(uint32_t* __restrict__ dat
     const int dist = 1 << (K - 1 - k);       // register distance
     const uint64_t twbase = 1ull << logh;    // stage table: w_{2h}^t = tw[h + t]
 #pragma unroll
-    for (int r = 0; r < (1 << K); r++) {
-      if (r & dist) continue;
-      const uint64_t t = lo + ((uint64_t)(r & (dist - 1)) << logd);
+    for (int j = 0; j < (1 << (K - 1)); j++) {
+      // j-th butterfly of this stage: register pair (r, r + dist), r has bit (K-1-k) clear
+      const int r = ((j / dist) * 2 * dist) + (j % dist);
+      const uint64_t t = lo + ((uint64_t)(j % dist) << logd);
       fr a = x[r], b = x[r + dist];
       x[r] = a + b;
       fr diff = a - b;
@@ -107,9 +108,9 @@ __global__ void __launch_bounds__(256) k_ntt_dit_pass(uint32_t* __restrict__ dat
     const int dist = 1 << k;
     const uint64_t twbase = 1ull << s;       // stage table: w_{2h}^t = tw[h + t], h = 2^s
 #pragma unroll
-    for (int r = 0; r < (1 << K); r++) {
-      if (r & dist) continue;
-      const uint64_t t = lo + ((uint64_t)(r & (dist - 1)) << logd);
+    for (int j = 0; j < (1 << (K - 1)); j++) {
+      const int r = ((j / dist) * 2 * dist) + (j % dist);
+      const uint64_t t = lo + ((uint64_t)(j % dist) << logd);
       fr a = x[r], b = x[r + dist];
       if (t) b = b * fr::load(tw + 8 * (twbase + t));
       x[r] = a + b;
