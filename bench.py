@@ -8,7 +8,7 @@ resident in HBM (kgs_prove_device). The SRS is a synthetic ptau of power 20 (tau
 keccak256("kgs-bench-tau") mod r) generated on the GPU by the product's own writer; SRS load and
 MSM-table precompute happen once, before the timed region (the device SRS cache).
 
-Per GPU, `--inflight` (default 2) independent proofs are in flight: one context (own HIP stream,
+Per GPU, `--inflight` (default 4) independent proofs are in flight: one context (own HIP stream,
 resident SRS copy, buffers) and one host thread each, so the latency-bound MSM tails and the host
 sync points of one proof overlap the bulk kernels of another; `latency_ms_single_proof` is the
 one-at-a-time latency on a single context, measured outside the timed region.
@@ -67,15 +67,18 @@ def bench_tau():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--nbits", type=int, default=20)
     ap.add_argument("--kind", choices=["grandsum", "grandproduct"], default="grandsum")
     ap.add_argument("--npols", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--msm-reps", type=int, default=5)
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--shard-proofs", type=int, default=3,
+                    help="N > 1: also time this many proofs with every MSM point-range sharded over all ranks "
+                         "(RCCL all-gather of the partials; 0 = skip)")
+    ap.add_argument("--inflight", type=int, default=4,
                     help="independent proofs in flight per GPU (one context + HIP stream + host thread each)")
     args = ap.parse_args()
 
@@ -167,6 +170,40 @@ def main():
     value = total_proofs / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
+    # ---------------- sharded leg (N > 1): one proof at a time over all GPUs, MSMs point-range
+    # sharded, NTT/elementwise work replicated; same inputs on every rank
+    sharded = None
+    if dist and args.shard_proofs > 0:
+        d_f = bufs[0][0]
+        d_t = bufs[0][1]
+        for i in range(args.npols):
+            keep[2 * i].copy_(torch.from_numpy(synth_evals(n, 4242 + i)[0].reshape(-1).copy()))
+            keep[2 * i + 1].copy_(torch.from_numpy(synth_evals(n, 4242 + i)[1].reshape(-1).copy()))
+        torch.cuda.synchronize()
+        ctx.set_shard(rank, world, K.torch_allgather(device=f"cuda:{local}"))
+        ctx.prove_device(kind, nbits, d_f, d_t)  # warm-up
+        dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.shard_proofs):
+            coms_sh = ctx.prove_device(kind, nbits, d_f, d_t)[0]
+        torch.cuda.synchronize()
+        dist.barrier()
+        el = time.perf_counter() - t1
+        te = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        el = float(te.item())
+        # all ranks must hold the same proof
+        h = torch.tensor(list(K.keccak256(b"".join(coms_sh))[:8]), dtype=torch.int64, device=f"cuda:{local}")
+        hs = [torch.empty_like(h) for _ in range(world)]
+        dist.all_gather(hs, h)
+        ctx.set_shard(0, 1)
+        sharded = {"n_gpus": world, "proofs": args.shard_proofs, "ms_per_proof": round(1000.0 * el / args.shard_proofs, 3),
+                   "proofs_per_s": round(args.shard_proofs / el, 4),
+                   "latency_speedup_vs_1gpu": round(latency_ms / (1000.0 * el / args.shard_proofs), 3),
+                   "ranks_agree": all(bool(torch.equal(hs[0], x)) for x in hs),
+                   "scaling": "strong (one proof split over all GPUs)"}
+
     if rank != 0:
         if dist:
             dist.barrier()
@@ -249,6 +286,7 @@ def main():
         "round_ms_single_proof": [round(x, 3) for x in rounds],
         "msm": msm,
         "roofline": roofline,
+        "sharded_msm": sharded,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out))

@@ -35,6 +35,7 @@ extern "C" {
 #define KGS_E_DOES_NOT_DIVIDE (-5) /* "Polynomial does not divide" (polynomial.js:847) */
 #define KGS_E_IO (-6)              /* ptau read/write failure (binfileutils / ptau_utils.js:3-24) */
 #define KGS_E_SRS (-7)             /* "The Powers of Tau file is not sufficiently large ..." (prover.js:79-81) */
+#define KGS_E_COMM (-8)            /* the shard all-gather callback reported a failure */
 
 #define KGS_GRANDSUM 0
 #define KGS_GRANDPRODUCT 1
@@ -47,6 +48,24 @@ const char* kgs_version(void);
 /* Create / destroy a context on HIP device `device`. */
 int kgs_ctx_create(int device, kgs_ctx_t** out);
 void kgs_ctx_destroy(kgs_ctx_t* ctx);
+
+/* ---- multi-GPU: MSM point-range sharding (replaces the [ffjs] worker-pool split
+ * of G1.multiExpAffine, polynomial.js:1106-1115, by a split over one process per GPU).
+ * With world > 1 every rank runs the whole prover on identical inputs; each commitment MSM over N
+ * points is cut into `world` contiguous point ranges (kgs_shard_range), rank r runs Pippenger on
+ * its range against the same resident SRS tables and the per-rank partials (c bit-sum points
+ * T_k, XYZZ, 128 B each) are exchanged through `fn`, once per prover round. Every rank then
+ * holds the same proof. `fn(user, send, recv, bytes)` must all-gather `bytes` from every rank
+ * into recv (rank-major, world * bytes) and return 0; it is called in the same order on every
+ * rank (the Python binding implements it over torch.distributed, i.e. RCCL on MI355X).
+ * world == 1 turns sharding off. */
+typedef int (*kgs_allgather_fn)(void* user, const uint8_t* send, uint8_t* recv, uint64_t bytes);
+int kgs_ctx_set_shard(kgs_ctx_t* ctx, int rank, int world, kgs_allgather_fn fn, void* user);
+/* rank's point range [lo, hi) of an n-point MSM: lo = floor(n*rank/world) */
+int kgs_shard_range(uint64_t n, int rank, int world, uint64_t* lo, uint64_t* hi);
+/* host-only: commitment from `nparts` rank partials (each c XYZZ points T_0..T_{c-1}, 128 B:
+ * X,Y,ZZ,ZZZ LE Montgomery Fq, ZZ == 0 is infinity): sum_k 2^k sum_r T_k^(r) -> affine LEM */
+int kgs_msm_combine(const uint8_t* T_all, int nparts, int c, uint8_t out_lem[64]);
 
 /* Load a .ptau file (binfileutils layout, sections 1-3) and make the first 2^(nbits_max+1) G1
  * points device-resident, together with the MSM window tables and the NTT tables for domains

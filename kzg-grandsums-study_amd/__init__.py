@@ -77,8 +77,16 @@ def lib():
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
         L.kgs_bench_ntt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_double)]
+        L.kgs_ctx_set_shard.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.kgs_shard_range.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(ctypes.c_uint64)]
+        L.kgs_msm_combine.argtypes = [c_u8p, ctypes.c_int, ctypes.c_int, c_u8p]
         _lib = L
     return _lib
+
+
+# int (*kgs_allgather_fn)(void* user, const uint8_t* send, uint8_t* recv, uint64_t bytes)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
 
 
 def _check(rc):
@@ -98,6 +106,59 @@ def keccak256(data: bytes) -> bytes:
     src = ctypes.create_string_buffer(bytes(data), max(1, len(data)))
     _check(lib().kgs_keccak256(src, len(data), out))
     return out.raw
+
+
+def shard_range(n, rank, world):
+    """Point range [lo, hi) of an n-point MSM owned by `rank` (kgs_shard_range)."""
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().kgs_shard_range(n, rank, world, ctypes.byref(lo), ctypes.byref(hi)))
+    return lo.value, hi.value
+
+
+def msm_combine(T_all, nparts, c):
+    """Commitment (64 B affine LEM) from `nparts` rank partials of c XYZZ bit-sum points each."""
+    if len(T_all) != nparts * c * 128:
+        raise ValueError("T_all must hold nparts * c * 128 bytes")
+    out = ctypes.create_string_buffer(64)
+    _check(lib().kgs_msm_combine(_buf(T_all), nparts, c, out))
+    return out.raw
+
+
+def torch_allgather(group=None, device=None):
+    """All-gather transport for Context.set_shard over torch.distributed: RCCL (backend "nccl")
+    when `device` is a GPU, gloo on host tensors otherwise."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+
+    def fn(data):
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        if device is not None:
+            t = t.to(device)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t, group=group)
+        return b"".join(o.cpu().numpy().tobytes() for o in outs)
+    return fn
+
+
+class ThreadGroup:
+    """In-process all-gather between `world` contexts driven by `world` host threads (one rank
+    each): several GPUs of one process, or the sharded path rehearsed on a single GPU."""
+
+    def __init__(self, world):
+        import threading
+        self.world = world
+        self._bar = threading.Barrier(world)
+        self._slots = [None] * world
+
+    def allgather(self, rank):
+        def fn(data):
+            self._slots[rank] = bytes(data)
+            self._bar.wait()
+            out = b"".join(self._slots)
+            self._bar.wait()
+            return out
+        return fn
 
 
 class Evaluations:
@@ -144,6 +205,27 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+    def set_shard(self, rank, world, allgather=None):
+        """MSM point-range sharding (kgs_ctx_set_shard): `allgather(bytes) -> world * bytes`
+        (rank-major), called in the same order on every rank. world == 1 switches it off."""
+        if world > 1 and allgather is None:
+            raise ValueError("sharding needs an all-gather transport")
+
+        def _cb(user, send, recv, nbytes):
+            try:
+                out = allgather(ctypes.string_at(send, nbytes))
+                if len(out) != nbytes * world:
+                    return -1
+                ctypes.memmove(recv, out, len(out))
+                return 0
+            except Exception:  # reported to the caller as KGS_E_COMM
+                import traceback
+                traceback.print_exc()
+                return -1
+        self._shard_cb = ALLGATHER_FN(_cb) if world > 1 else None
+        fp = ctypes.cast(self._shard_cb, ctypes.c_void_p) if world > 1 else None
+        _check(lib().kgs_ctx_set_shard(self._h, rank, world, fp, None))
 
     def load_ptau(self, path, nbits_max=-1):
         _check(lib().kgs_srs_load_ptau(self._h, os.fsencode(path), nbits_max))

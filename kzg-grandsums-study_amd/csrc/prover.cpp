@@ -120,6 +120,10 @@ struct kgs_ctx {
   uint32_t *tw_fwd = nullptr, *tw_inv = nullptr, *coset_pow = nullptr, *coset_ipow = nullptr, *invm = nullptr;
   std::map<std::pair<int, int>, uint32_t*> nxm1;  // (nbits, lcs) -> 1/(n(x-1)) on the coset (bitrev)
   std::vector<double> timing;
+  // MSM point-range sharding (kgs_ctx_set_shard): world > 1 splits every commitment MSM
+  int shard_rank = 0, shard_world = 1;
+  kgs_allgather_fn shard_fn = nullptr;
+  void* shard_user = nullptr;
 
   ~kgs_ctx() {
     hipSetDevice(device);
@@ -301,10 +305,18 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
 }
 
 // ------------------------------------------------------------------ MSM (commit)
+// Polynomial.multiExponentiation (polynomial.js:1106-1115): device Pippenger -> c bit-sum points
+// T_k (XYZZ) -> host sum_k 2^k T_k -> affine LEM. Sharded (world > 1): this rank's point range
+// only; the partials of all ranks are all-gathered once per batch of commits (one prover round).
 struct Commit {
-  uint8_t* h_T = nullptr;  // pinned, c x 128 B
+  uint8_t* h_T = nullptr;  // pinned, c x 128 B (this rank's partial)
   uint64_t N = 0;
 };
+
+void shard_range(uint64_t n, int rank, int world, uint64_t& lo, uint64_t& hi) {
+  lo = (uint64_t)((unsigned __int128)n * (unsigned)rank / (unsigned)world);
+  hi = (uint64_t)((unsigned __int128)n * (unsigned)(rank + 1) / (unsigned)world);
+}
 
 Commit commit_launch(kgs_ctx& c, const uint32_t* scalars, uint64_t N, int slot) {
   Commit cm;
@@ -312,29 +324,59 @@ Commit commit_launch(kgs_ctx& c, const uint32_t* scalars, uint64_t N, int slot) 
   const int cc = c.tb.c;
   uint32_t* dT = c.buf("msm_T", (size_t)64 * cc * 128) + (size_t)slot * cc * 32;
   if (N > c.tb.npts) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
+  if (slot >= 64) throw KgsError(KGS_E_ARG, "too many commitments in flight");
   cm.h_T = c.pin((size_t)cc * 128);
-  if (N == 0) {
-    memset(cm.h_T, 0, (size_t)cc * 128);
+  uint64_t lo = 0, hi = N;
+  if (c.shard_world > 1) shard_range(N, c.shard_rank, c.shard_world, lo, hi);
+  if (hi == lo) {
+    memset(cm.h_T, 0, (size_t)cc * 128);  // ZZ == 0: infinity
     return cm;
   }
-  msm_run(c.st, c.tb, c.mw, scalars, N, dT);
+  MsmTables tb = c.tb;
+  tb.table += (size_t)16 * lo;  // same window stride (npts), points [lo, hi)
+  msm_run(c.st, tb, c.mw, scalars + (size_t)8 * lo, hi - lo, dT);
   check_launch();
   HC(hipMemcpyAsync(cm.h_T, dT, (size_t)cc * 128, hipMemcpyDeviceToHost, c.st));
   return cm;
 }
 
-// after sync: sum_k 2^k T_k -> affine LEM
-void commit_finish(kgs_ctx& c, const Commit& cm, uint8_t out[64]) {
-  const int cc = c.tb.c;
+// sum_k 2^k sum_r T_k^(r) -> affine LEM
+void combine_partials(const uint8_t* T_all, size_t part_stride, int nparts, int cc, uint8_t out[64]) {
   host::G1 acc = host::G1::inf();
-  if (cm.N) {
-    for (int k = cc - 1; k >= 0; k--) {
-      acc = acc.dbl();
-      acc = acc.add(host::G1::from_bytes128(cm.h_T + 128 * k));
-    }
+  for (int k = cc - 1; k >= 0; k--) {
+    acc = acc.dbl();
+    for (int r = 0; r < nparts; r++) acc = acc.add(host::G1::from_bytes128(T_all + r * part_stride + 128 * k));
   }
   acc.to_affine_lem(out);
 }
+
+// after sync: finish a batch of commits (one all-gather per batch when sharded)
+void commits_finish(kgs_ctx& c, const std::vector<Commit>& cms, std::vector<uint8_t*> outs) {
+  const int cc = c.tb.c;
+  const size_t tb = (size_t)cc * 128;
+  const int world = c.shard_world;
+  bool any = false;
+  for (auto& cm : cms) any |= cm.N > 0;
+  if (world == 1 || !any) {
+    for (size_t i = 0; i < cms.size(); i++) {
+      if (cms[i].N) combine_partials(cms[i].h_T, tb, 1, cc, outs[i]);
+      else host::G1::inf().to_affine_lem(outs[i]);
+    }
+    return;
+  }
+  const size_t bytes = tb * cms.size();
+  std::vector<uint8_t> send(bytes), recv(bytes * world);
+  for (size_t i = 0; i < cms.size(); i++) memcpy(send.data() + i * tb, cms[i].h_T, tb);
+  if (!c.shard_fn) throw KgsError(KGS_E_COMM, "sharding enabled without an all-gather callback");
+  if (c.shard_fn(c.shard_user, send.data(), recv.data(), bytes) != 0)
+    throw KgsError(KGS_E_COMM, "shard all-gather failed");
+  for (size_t i = 0; i < cms.size(); i++) {
+    if (cms[i].N) combine_partials(recv.data() + i * tb, bytes, world, cc, outs[i]);
+    else host::G1::inf().to_affine_lem(outs[i]);
+  }
+}
+
+void commit_finish(kgs_ctx& c, const Commit& cm, uint8_t out[64]) { commits_finish(c, {cm}, {out}); }
 
 // ------------------------------------------------------------------ Horner evaluation
 // returns p_j(x) for each poly of the batch
@@ -475,7 +517,11 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   const int ncom = 2 * k + (sel ? 2 : 0) + 4;
   std::vector<std::vector<uint8_t>> com(ncom, std::vector<uint8_t>(64));
   int ci = 0;
-  for (auto& cm : r1) commit_finish(c, cm, com[ci++].data());
+  {
+    std::vector<uint8_t*> outs;
+    for (size_t i = 0; i < r1.size(); i++) outs.push_back(com[ci++].data());
+    commits_finish(c, r1, outs);
+  }
   lap(0);
 
   // ---------------- round 2: challenges, combined polynomials, S / Z (prover.js:181-231)
@@ -710,8 +756,8 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   HC(hipMemcpyAsync(h_flags, flags, 64, hipMemcpyDeviceToHost, c.st));
   c.sync();
   if (h_flags[2] || h_flags[3]) throw KgsError(KGS_E_DOES_NOT_DIVIDE, "Polynomial does not divide");
-  commit_finish(c, cW1, com[ci++].data());
-  commit_finish(c, cW2, com[ci++].data());
+  commits_finish(c, {cW1, cW2}, {com[ci].data(), com[ci + 1].data()});
+  ci += 2;
   lap(4);
 
   for (int i = 0; i < ncom; i++) memcpy(com_out + 64 * i, com[i].data(), 64);
@@ -1139,6 +1185,32 @@ int kgs_msm(kgs_ctx_t* ctx, const uint8_t* scalars_mont, uint64_t n, uint8_t out
   ctx->sync();
   commit_finish(*ctx, cm, out_lem);
   ctx->reset_staging();
+  API_END
+}
+
+int kgs_ctx_set_shard(kgs_ctx_t* ctx, int rank, int world, kgs_allgather_fn fn, void* user) {
+  API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "ctx is NULL");
+  if (world < 1 || rank < 0 || rank >= world) throw KgsError(KGS_E_ARG, "bad shard rank/world");
+  if (world > 1 && !fn) throw KgsError(KGS_E_ARG, "sharding needs an all-gather callback");
+  ctx->shard_rank = world > 1 ? rank : 0;
+  ctx->shard_world = world;
+  ctx->shard_fn = world > 1 ? fn : nullptr;
+  ctx->shard_user = world > 1 ? user : nullptr;
+  API_END
+}
+
+int kgs_shard_range(uint64_t n, int rank, int world, uint64_t* lo, uint64_t* hi) {
+  API_BEGIN
+  if (world < 1 || rank < 0 || rank >= world || !lo || !hi) throw KgsError(KGS_E_ARG, "bad shard rank/world");
+  shard_range(n, rank, world, *lo, *hi);
+  API_END
+}
+
+int kgs_msm_combine(const uint8_t* T_all, int nparts, int c, uint8_t out_lem[64]) {
+  API_BEGIN
+  if (!T_all || !out_lem || nparts < 1 || c < 1 || c > 32) throw KgsError(KGS_E_ARG, "bad msm_combine arguments");
+  combine_partials(T_all, (size_t)c * 128, nparts, c, out_lem);
   API_END
 }
 

@@ -249,3 +249,123 @@ def test_mid_size_vs_c_oracle(K, kind, nbits, npols, sel):
     ecoms, eevs = C.prove_raw(kk, nbits, Fs, Ts, sF, sT, srs, 0)
     assert coms == ecoms and evs == eevs
     ctx.close()
+
+
+def _sharded_run(K, world, ptau, nbits, kind, Fs, Ts, sF, sT):
+    """`world` contexts (one per simulated rank, all on cuda:0), one host thread each, MSMs
+    point-range sharded through an in-process all-gather. Returns every rank's proof."""
+    import threading
+    grp = K.ThreadGroup(world)
+    ctxs = [K.Context(0) for _ in range(world)]
+    for r, c in enumerate(ctxs):
+        c.load_ptau(ptau, nbits)
+        c.set_shard(r, world, grp.allgather(r))
+    out, err = [None] * world, [None] * world
+
+    def run(r):
+        try:
+            out[r] = ctxs[r].prove(kind, nbits, Fs, Ts, sF, sT, mont_out=False)[:2]
+        except Exception as e:  # pragma: no cover
+            err[r] = e
+            grp._bar.abort()
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    for c in ctxs:
+        c.close()
+    assert not any(err), err
+    return out
+
+
+@pytest.mark.parametrize("kind,nbits,npols,sel,world", [("grandsum", 9, 1, False, 2), ("grandproduct", 9, 2, True, 3),
+                                                        ("grandsum", 4, 1, True, 8)])
+def test_sharded_prover_matches_golden_path(K, kind, nbits, npols, sel, world):
+    """MSM point-range sharding (kgs_ctx_set_shard): every rank's proof equals the unsharded one."""
+    ptau = common.oracle_ptau(max(nbits, 9))
+    Fs, Ts, sF, sT = common.make_inputs(900 + nbits + world, nbits, npols, sel)
+    kk = K.GRANDSUM if kind == "grandsum" else K.GRANDPRODUCT
+    ctx = K.Context(0)
+    ctx.load_ptau(ptau, nbits)
+    want = ctx.prove(kk, nbits, Fs, Ts, sF, sT, mont_out=False)[:2]
+    ctx.close()
+    got = _sharded_run(K, world, ptau, nbits, kk, Fs, Ts, sF, sT)
+    for r in range(world):
+        assert got[r] == want, r
+
+
+def test_sharded_prover_large(K):
+    """2^16 grand-sum k=2, 2 ranks: sharded proof == unsharded proof, and it verifies."""
+    nbits = 16
+    path = f"/tmp/kgs_test_gpu_p{nbits}.ptau"
+    ctx = K.Context(0)
+    if not os.path.exists(path):
+        ctx.write_synthetic_ptau(path, nbits, common.tau())
+    ctx.load_ptau(path, nbits)
+    Fs, Ts, sF, sT = common.make_inputs(4242, nbits, 2, False)
+    want = ctx.prove(K.GRANDSUM, nbits, Fs, Ts, sF, sT, mont_out=False)[:2]
+    ctx.close()
+    got = _sharded_run(K, 2, path, nbits, K.GRANDSUM, Fs, Ts, sF, sT)
+    assert got[0] == want and got[1] == want
+
+
+def test_shard_callback_failure_is_reported(K):
+    ctx = K.Context(0)
+    ctx.load_ptau(common.oracle_ptau(9), 4)
+
+    def bad(data):
+        raise RuntimeError("transport down")
+    ctx.set_shard(0, 2, bad)
+    Fs, Ts, sF, sT = common.make_inputs(5, 4, 1, False)
+    with pytest.raises(K.KgsError) as ei:
+        ctx.prove(K.GRANDSUM, 4, Fs, Ts, sF, sT, mont_out=False)
+    assert ei.value.code == -8
+    ctx.set_shard(0, 1)
+    ctx.prove(K.GRANDSUM, 4, Fs, Ts, sF, sT, mont_out=False)
+    ctx.close()
+
+
+def _gloo_prover_rank(rank, world, port, ptau, q):
+    try:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        K = common.load_pkg()
+        ctx = K.Context(0)
+        ctx.load_ptau(ptau, 10)
+        ctx.set_shard(rank, world, K.torch_allgather())
+        Fs, Ts, sF, sT = common.make_inputs(31337, 10, 2, True)
+        coms, evs = ctx.prove(K.GRANDSUM, 10, Fs, Ts, sF, sT, mont_out=False)[:2]
+        ctx.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, coms, evs))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, None, repr(e)))
+
+
+def test_sharded_prover_two_processes(K):
+    """one process per rank (as under torchrun), torch.distributed transport (gloo host tensors)"""
+    import multiprocessing as mp
+    import socket
+    ptau = common.oracle_ptau(11)
+    ctx = K.Context(0)
+    ctx.load_ptau(ptau, 10)
+    Fs, Ts, sF, sT = common.make_inputs(31337, 10, 2, True)
+    want = ctx.prove(K.GRANDSUM, 10, Fs, Ts, sF, sT, mont_out=False)[:2]
+    ctx.close()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    procs = [mpc.Process(target=_gloo_prover_rank, args=(r, 2, port, ptau, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, coms, evs in res:
+        assert coms is not None, evs
+        assert (coms, evs) == want, rank
