@@ -76,51 +76,84 @@ void msm_build_table(hipStream_t st, uint32_t* table, uint64_t npts, int c, int 
 // ------------------------------------------------------------------ digits + two-pass bucket sort
 // Entry (j, i) = (window, point) with signed digit d = digit_j(from_mont(scalar_i)); key |d| in
 // [0, B], B = 2^(c-1); key 0 entries are dropped. Sort by key without global per-entry atomics:
-//  pass 1 partitions by hi = key >> LOB (NH <= 257 partitions; LDS histogram + one global
-//          reservation per (block, partition)); digits are RECOMPUTED from the scalars instead of
-//          being materialised (one Montgomery product per scalar);
-//  pass 2 sorts every partition by lo = key & (2^LOB - 1) inside one workgroup (LDS histogram,
-//          LDS cursors) and writes the bucket offsets.
+//  pass 1 partitions by p = min(key >> LOB, NH - 1) (NH = B >> LOB <= 256 partitions; the last
+//          one also holds key B). Per-block partition counts come from a histogram pass whose
+//          block x partition table is scanned; each block then counting-sorts its entries in LDS
+//          and writes them out as contiguous per-partition runs (coalesced stores instead of one
+//          scattered 4 B + 1 B store per entry). Digits are RECOMPUTED from the scalars in both
+//          passes instead of being materialised (one Montgomery product per scalar);
+//  pass 2 sorts every partition by lo = key - (p << LOB) inside one workgroup, tile by tile
+//          through LDS (again run-wise stores), and writes the bucket offsets.
 // Order inside a bucket is unspecified (point addition is commutative).
-__device__ __forceinline__ void scalar_digits(int32_t* d, const uint32_t* sc, uint64_t i, int c, int W) {
+template <int C>
+__device__ __forceinline__ void scalar_digits(int32_t (&d)[(255 + C - 1) / C], const uint32_t* sc, uint64_t i) {
+  constexpr int W = (255 + C - 1) / C;
   fr s = fr::load(sc + 8 * i).from_mont();
-  const int32_t half = 1 << (c - 1);
-  const uint32_t mask = (1u << c) - 1;
+  constexpr int32_t half = 1 << (C - 1);
+  constexpr uint32_t mask = (1u << C) - 1;
   uint32_t carry = 0;
+#pragma unroll
   for (int j = 0; j < W; j++) {
-    const int bit = j * c;
+    const int bit = j * C;
     const int limb = bit >> 5, off = bit & 31;
     uint64_t w = limb < 8 ? s.v[limb] : 0;
     if (limb + 1 < 8) w |= (uint64_t)s.v[limb + 1] << 32;
     int32_t v = (int32_t)((w >> off) & mask) + (int32_t)carry;
-    if (v > half) {
-      v -= (1 << c);
-      carry = 1;
-    } else {
-      carry = 0;
-    }
-    d[j] = v;
+    carry = v > half ? 1u : 0u;
+    d[j] = carry ? v - (1 << C) : v;
   }
 }
 
-constexpr int MSM_WMAX = 43;  // windows for c >= 6
+// exclusive scan of a[0..n), n <= 256, by the 64 lanes of ONE wave (4 elements per lane); out may alias a
+__device__ __forceinline__ uint32_t wave_excl_scan256(const uint32_t* a, uint32_t* out, int n) {
+  const int lane = threadIdx.x & 63;
+  uint32_t x[4], local = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int idx = lane * 4 + k;
+    x[k] = idx < n ? a[idx] : 0;
+    local += x[k];
+  }
+  uint32_t incl = local;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off);
+    if (lane >= off) incl += y;
+  }
+  uint32_t run = incl - local;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int idx = lane * 4 + k;
+    if (idx < n) out[idx] = run;
+    run += x[k];
+  }
+  return __shfl(incl, 63);  // total
+}
 
+__device__ __forceinline__ uint32_t part_of(uint32_t key, int lob, int NH) {
+  const uint32_t p = key >> lob;
+  return p < (uint32_t)NH ? p : (uint32_t)NH - 1;
+}
+
+template <int C>
 __global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ bh, const uint32_t* __restrict__ sc,
-                                                   uint64_t N, int c, int W, int lob, int NH, uint32_t nblk) {
+                                                   uint64_t N, int lob, int NH, uint32_t nblk) {
   // per-block partition histogram, stored transposed: bh[p * nblk + block]
-  __shared__ uint32_t h[264];
-  for (int b = threadIdx.x; b < NH; b += 256) h[b] = 0;
+  constexpr int W = (255 + C - 1) / C;
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < N) {
-    int32_t d[MSM_WMAX];
-    scalar_digits(d, sc, i, c, W);
+    int32_t d[W];
+    scalar_digits<C>(d, sc, i);
+#pragma unroll
     for (int j = 0; j < W; j++) {
-      if (d[j]) atomicAdd(&h[(uint32_t)(d[j] < 0 ? -d[j] : d[j]) >> lob], 1u);
+      if (d[j]) atomicAdd(&h[part_of((uint32_t)(d[j] < 0 ? -d[j] : d[j]), lob, NH)], 1u);
     }
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < NH; b += 256) bh[(uint64_t)b * nblk + blockIdx.x] = h[b];
+  if ((int)threadIdx.x < NH) bh[(uint64_t)threadIdx.x * nblk + blockIdx.x] = h[threadIdx.x];
 }
 
 // grid = NH workgroups: exclusive scan of one partition's per-block counts (in place) and its total
@@ -149,71 +182,135 @@ __global__ void __launch_bounds__(256) k_sort_scan_blocks(uint32_t* __restrict__
   if (threadIdx.x == 255) ptot[blockIdx.x] = part[255];
 }
 
-// hi_off[p] = exclusive scan of partition totals; offsets[B+1] = total (single thread, NH <= 257)
-__global__ void k_sort_scan(uint32_t* __restrict__ hi_off, const uint32_t* __restrict__ ptot, int NH,
-                            uint32_t* __restrict__ offsets, uint32_t B) {
+// hi_off[p] = exclusive scan of partition totals (NH <= 256); offsets[B+1] = total
+__global__ void __launch_bounds__(64) k_sort_scan(uint32_t* __restrict__ hi_off, const uint32_t* __restrict__ ptot,
+                                                  int NH, uint32_t* __restrict__ offsets, uint32_t B) {
+  const uint32_t total = wave_excl_scan256(ptot, hi_off, NH);
   if (threadIdx.x == 0) {
-    uint32_t run = 0;
-    for (int p = 0; p < NH; p++) {
-      hi_off[p] = run;
-      run += ptot[p];
-    }
-    hi_off[NH] = run;
-    offsets[B + 1] = run;
+    hi_off[NH] = total;
+    offsets[B + 1] = total;
   }
 }
 
+// dynamic LDS: 256 * W * (4 + 2) bytes of staging
+template <int C>
 __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, uint8_t* __restrict__ tlo,
-                                                   const uint32_t* __restrict__ bh, const uint32_t* __restrict__ hi_off,
-                                                   const uint32_t* __restrict__ sc, uint64_t N, uint64_t Nsrs, int c,
-                                                   int W, int lob, int NH, uint32_t nblk) {
-  __shared__ uint32_t cnt[264];
-  __shared__ uint32_t base[264];
-  for (int b = threadIdx.x; b < NH; b += 256) {
-    cnt[b] = 0;
-    base[b] = hi_off[b] + bh[(uint64_t)b * nblk + blockIdx.x];
+                                                   const uint32_t* __restrict__ bh, const uint32_t* __restrict__ ptot,
+                                                   const uint32_t* __restrict__ hi_off, const uint32_t* __restrict__ sc,
+                                                   uint64_t N, uint64_t Nsrs, int lob, int NH, uint32_t nblk) {
+  constexpr int W = (255 + C - 1) / C;
+  extern __shared__ uint32_t smem[];
+  uint32_t* sval = smem;                             // 256 * W
+  uint16_t* skey = (uint16_t*)(smem + 256 * W);      // 256 * W (key <= 2^15)
+  __shared__ uint32_t base[256], loff[256], cur[256];
+  __shared__ uint32_t total;
+  const uint32_t blk = blockIdx.x, tid = threadIdx.x;
+  if ((int)tid < NH) {
+    const uint32_t mine = bh[(uint64_t)tid * nblk + blk];
+    const uint32_t nxt = blk + 1 < nblk ? bh[(uint64_t)tid * nblk + blk + 1] : ptot[tid];
+    base[tid] = hi_off[tid] + mine;
+    cur[tid] = nxt - mine;  // this block's count, scanned below
   }
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  int32_t d[MSM_WMAX];
-  scalar_digits(d, sc, i, c, W);
-  const uint32_t lomask = (1u << lob) - 1;
-  for (int j = 0; j < W; j++) {
-    if (!d[j]) continue;
-    const uint32_t k = (uint32_t)(d[j] < 0 ? -d[j] : d[j]);
-    const uint32_t pos = base[k >> lob] + atomicAdd(&cnt[k >> lob], 1u);
-    tval[pos] = (uint32_t)((uint64_t)j * Nsrs + i) | (d[j] < 0 ? 0x80000000u : 0u);
-    tlo[pos] = (uint8_t)(k & lomask);
+  if (tid < 64) {
+    const uint32_t t = wave_excl_scan256(cur, loff, NH);
+    if (tid == 0) total = t;
   }
-}
-
-// one workgroup per hi partition p: counting sort by lo, bucket offsets for keys (p << lob) + lo
-__global__ void __launch_bounds__(1024) k_sort_lo(uint32_t* __restrict__ sorted, uint32_t* __restrict__ offsets,
-                                                 const uint32_t* __restrict__ tval, const uint8_t* __restrict__ tlo,
-                                                 const uint32_t* __restrict__ hi_off, int lob, uint32_t B) {
-  __shared__ uint32_t cnt[256];
-  __shared__ uint32_t cur[256];
-  const int p = blockIdx.x;
-  const uint32_t nlo = 1u << lob;
-  const uint32_t s0 = hi_off[p], s1 = hi_off[p + 1];
-  for (uint32_t b = threadIdx.x; b < nlo; b += blockDim.x) cnt[b] = 0;
   __syncthreads();
-  for (uint32_t e = s0 + threadIdx.x; e < s1; e += blockDim.x) atomicAdd(&cnt[tlo[e]], 1u);
+  if ((int)tid < NH) cur[tid] = loff[tid];
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t run = s0;
-    for (uint32_t b = 0; b < nlo; b++) {
-      const uint32_t key = ((uint32_t)p << lob) + b;
-      cur[b] = run;
-      if (key <= B) offsets[key] = run;
-      run += cnt[b];
+  const uint64_t i = (uint64_t)blk * blockDim.x + tid;
+  if (i < N) {
+    int32_t d[W];
+    scalar_digits<C>(d, sc, i);
+#pragma unroll
+    for (int j = 0; j < W; j++) {
+      if (!d[j]) continue;
+      const uint32_t k = (uint32_t)(d[j] < 0 ? -d[j] : d[j]);
+      const uint32_t pos = atomicAdd(&cur[part_of(k, lob, NH)], 1u);
+      sval[pos] = (uint32_t)((uint64_t)j * Nsrs + i) | (d[j] < 0 ? 0x80000000u : 0u);
+      skey[pos] = (uint16_t)k;
     }
   }
   __syncthreads();
-  for (uint32_t e = s0 + threadIdx.x; e < s1; e += blockDim.x) {
-    const uint32_t pos = atomicAdd(&cur[tlo[e]], 1u);
-    sorted[pos] = tval[e];
+  const uint32_t tot = total;
+  for (uint32_t e = tid; e < tot; e += 256) {
+    const uint32_t k = skey[e];
+    const uint32_t p = part_of(k, lob, NH);
+    const uint32_t g = base[p] + (e - loff[p]);
+    tval[g] = sval[e];
+    tlo[g] = (uint8_t)(k - (p << lob));
+  }
+}
+
+// one workgroup per partition p: counting sort by lo (tiles of SL_TILE through LDS), bucket
+// offsets for keys (p << lob) + lo
+constexpr int SL_THREADS = 1024;
+constexpr int SL_TILE = 4096;
+__global__ void __launch_bounds__(SL_THREADS) k_sort_lo(uint32_t* __restrict__ sorted, uint32_t* __restrict__ offsets,
+                                                         const uint32_t* __restrict__ tval,
+                                                         const uint8_t* __restrict__ tlo,
+                                                         const uint32_t* __restrict__ hi_off, int lob, int NH,
+                                                         uint32_t B) {
+  __shared__ uint32_t cnt[256], cur[256], tcnt[256], toff[256];
+  __shared__ uint32_t sv[SL_TILE];
+  __shared__ uint8_t sl[SL_TILE];
+  const int p = blockIdx.x;
+  const uint32_t tid = threadIdx.x;
+  const int nb = (1 << lob) + (p == NH - 1 ? 1 : 0);  // the last partition also holds key B
+  const uint32_t s0 = hi_off[p], s1 = hi_off[p + 1];
+  if ((int)tid < nb) cnt[tid] = 0;
+  __syncthreads();
+  for (uint32_t e = s0 + tid; e < s1; e += SL_THREADS) atomicAdd(&cnt[tlo[e]], 1u);
+  __syncthreads();
+  if (tid < 64) {
+    wave_excl_scan256(cnt, cur, nb);
+    for (int b = tid; b < nb; b += 64) {
+      cur[b] += s0;
+      const uint32_t key = ((uint32_t)p << lob) + b;
+      if (key <= B) offsets[key] = cur[b];
+    }
+  }
+  __syncthreads();
+  for (uint32_t t0 = s0; t0 < s1; t0 += SL_TILE) {
+    const uint32_t tn = s1 - t0 < (uint32_t)SL_TILE ? s1 - t0 : (uint32_t)SL_TILE;
+    if ((int)tid < nb) tcnt[tid] = 0;
+    __syncthreads();
+    uint32_t v[SL_TILE / SL_THREADS], r[SL_TILE / SL_THREADS];
+    uint8_t l[SL_TILE / SL_THREADS];
+#pragma unroll
+    for (int k = 0; k < SL_TILE / SL_THREADS; k++) {
+      const uint32_t e = tid + k * SL_THREADS;
+      if (e < tn) {
+        l[k] = tlo[t0 + e];
+        v[k] = tval[t0 + e];
+        r[k] = atomicAdd(&tcnt[l[k]], 1u);
+      }
+    }
+    __syncthreads();
+    if (tid < 64) wave_excl_scan256(tcnt, toff, nb);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SL_TILE / SL_THREADS; k++) {
+      const uint32_t e = tid + k * SL_THREADS;
+      if (e < tn) {
+        const uint32_t q = toff[l[k]] + r[k];
+        sv[q] = v[k];
+        sl[q] = l[k];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SL_TILE / SL_THREADS; k++) {
+      const uint32_t e = tid + k * SL_THREADS;
+      if (e < tn) {
+        const uint32_t b = sl[e];
+        sorted[cur[b] + (e - toff[b])] = sv[e];
+      }
+    }
+    __syncthreads();
+    if ((int)tid < nb) cur[tid] += tcnt[tid];
+    __syncthreads();
   }
 }
 
@@ -263,58 +360,92 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
   emit_run(bstart, segpart, b, rs, offsets, s, acc);
 }
 
+// bucket b = bstart[b] + the segment partials of the segments starting strictly inside it; two
+// lanes per bucket (even / odd segments), joined by one xor-shuffle add
+__device__ __forceinline__ g1_xyzz shfl_xor_pt(const g1_xyzz& a, int mask) {
+  g1_xyzz r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r.X.v[i] = __shfl_xor(a.X.v[i], mask);
+    r.Y.v[i] = __shfl_xor(a.Y.v[i], mask);
+    r.ZZ.v[i] = __shfl_xor(a.ZZ.v[i], mask);
+    r.ZZZ.v[i] = __shfl_xor(a.ZZZ.v[i], mask);
+  }
+  return r;
+}
+
 __global__ void __launch_bounds__(256) k_combine(uint32_t* __restrict__ buckets, const uint32_t* __restrict__ bstart,
                                                  const uint32_t* __restrict__ segpart,
                                                  const uint32_t* __restrict__ offsets, uint32_t B, uint32_t L) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x + 1;  // buckets 1..B
-  if (b > B) return;
-  const uint64_t o0 = offsets[b], o1 = offsets[b + 1];
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t b = (g >> 1) + 1;  // buckets 1..B
+  const uint32_t sub = g & 1;
   g1_xyzz acc = g1_xyzz::inf();
-  if (o1 > o0) {
-    acc = g1_xyzz::load(bstart + 32 * (uint64_t)b);
-    for (uint64_t sgm = o0 / L + 1; sgm * L < o1; sgm++) acc.add(g1_xyzz::load(segpart + 32 * sgm));
+  if (b <= B) {
+    const uint64_t o0 = offsets[b], o1 = offsets[b + 1];
+    if (o1 > o0) {
+      if (sub == 0) acc = g1_xyzz::load(bstart + 32 * (uint64_t)b);
+      for (uint64_t sgm = o0 / L + 1 + sub; sgm * L < o1; sgm += 2) acc.add(g1_xyzz::load(segpart + 32 * sgm));
+    }
   }
-  acc.store(buckets + 32 * (uint64_t)b);
+  acc.add(shfl_xor_pt(acc, 1));
+  if (b <= B && sub == 0) acc.store(buckets + 32 * (uint64_t)b);
 }
 
 // ------------------------------------------------------------------ sum_b b*S_b via bit sums
-// block (k, chunk): tree-sum of the buckets b in [1, B-1] with bit k set (k < c-1), t-th such
-// bucket: insert a 1 at bit k of t. k == c-1: bucket B alone.
+// T_k = sum of the buckets b in [1, B-1] with bit k set (k < c-1; the t-th such bucket: insert a
+// 1 at bit k of t), T_{c-1} = S_B. Block (chunk, k): every thread first adds BS_CHAIN buckets in
+// sequence (all lanes busy), then one LDS tree over the 256 thread sums (the active lanes stay
+// packed in the low waves, so the tree costs ~9 wave-adds instead of 6 per wave with shuffles).
+constexpr int BS_CHAIN = 8;
+constexpr uint32_t BS_SPAN = 256 * BS_CHAIN;  // buckets per block
+
+__device__ __forceinline__ g1_xyzz block_tree_sum256(g1_xyzz v, uint32_t* lds) {
+  for (int stride = 128; stride > 0; stride >>= 1) {
+    if (threadIdx.x >= stride && threadIdx.x < 2 * stride) v.store(lds + 32 * (threadIdx.x - stride));
+    __syncthreads();
+    if (threadIdx.x < stride) v.add(g1_xyzz::load(lds + 32 * threadIdx.x));
+    __syncthreads();
+  }
+  return v;
+}
+
 __global__ void __launch_bounds__(256) k_bitsum1(uint32_t* __restrict__ part, const uint32_t* __restrict__ buckets,
                                                  int c, uint32_t chunks) {
-  __shared__ uint32_t lds[256 * 32];
+  __shared__ uint32_t lds[128 * 32];
   const int k = blockIdx.y;
   const uint32_t chunk = blockIdx.x;
   const uint32_t B = 1u << (c - 1);
-  const uint32_t t = chunk * 256 + threadIdx.x;
   g1_xyzz v = g1_xyzz::inf();
   if (k == c - 1) {
-    if (t == 0) v = g1_xyzz::load(buckets + 32 * (uint64_t)B);
-  } else if (t < B / 2) {
-    uint32_t b = ((t >> k) << (k + 1)) | (1u << k) | (t & ((1u << k) - 1));
-    v = g1_xyzz::load(buckets + 32 * (uint64_t)b);
+    if (chunk == 0 && threadIdx.x == 0) v = g1_xyzz::load(buckets + 32 * (uint64_t)B);
+  } else {
+#pragma unroll 1
+    for (int i = 0; i < BS_CHAIN; i++) {
+      const uint32_t t = chunk * BS_SPAN + i * 256 + threadIdx.x;
+      if (t < B / 2) {
+        const uint32_t b = ((t >> k) << (k + 1)) | (1u << k) | (t & ((1u << k) - 1));
+        v.add(g1_xyzz::load(buckets + 32 * (uint64_t)b));
+      }
+    }
   }
-  for (int stride = 128; stride > 0; stride >>= 1) {
-    if (threadIdx.x >= stride && threadIdx.x < 2 * stride) v.store(lds + 32 * (threadIdx.x - stride));
-    __syncthreads();
-    if (threadIdx.x < stride) v.add(g1_xyzz::load(lds + 32 * threadIdx.x));
-    __syncthreads();
+  if (k == c - 1 && chunk > 0) {  // uniform per block: an empty partial
+    if (threadIdx.x == 0) v.store(part + 32 * ((uint64_t)k * chunks + chunk));
+    return;
   }
+  v = block_tree_sum256(v, lds);
   if (threadIdx.x == 0) v.store(part + 32 * ((uint64_t)k * chunks + chunk));
 }
 
-__global__ void __launch_bounds__(256) k_bitsum2(uint32_t* __restrict__ T, const uint32_t* __restrict__ part,
-                                                 uint32_t chunks) {
-  __shared__ uint32_t lds[256 * 32];
+// one wave per k: sum the chunk partials (<= 64 per lane pass), xor-shuffle tree
+__global__ void __launch_bounds__(64) k_bitsum2(uint32_t* __restrict__ T, const uint32_t* __restrict__ part,
+                                                uint32_t chunks) {
   const int k = blockIdx.x;
   g1_xyzz v = g1_xyzz::inf();
-  for (uint32_t i = threadIdx.x; i < chunks; i += 256) v.add(g1_xyzz::load(part + 32 * ((uint64_t)k * chunks + i)));
-  for (int stride = 128; stride > 0; stride >>= 1) {
-    if (threadIdx.x >= stride && threadIdx.x < 2 * stride) v.store(lds + 32 * (threadIdx.x - stride));
-    __syncthreads();
-    if (threadIdx.x < stride) v.add(g1_xyzz::load(lds + 32 * threadIdx.x));
-    __syncthreads();
-  }
+  for (uint32_t i = threadIdx.x; i < chunks; i += 64) v.add(g1_xyzz::load(part + 32 * ((uint64_t)k * chunks + i)));
+  uint32_t width = 1;
+  while (width < chunks && width < 64) width <<= 1;
+  for (uint32_t m = width >> 1; m > 0; m >>= 1) v.add(shfl_xor_pt(v, m));
   if (threadIdx.x == 0) v.store(T + 32 * (uint64_t)k);
 }
 
@@ -327,18 +458,29 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   const int c = tb.c, W = tb.W;
   const uint32_t B = 1u << (c - 1);
   const int lob = c - 1 < 7 ? c - 1 : 7;
-  const int NH = (int)(B >> lob) + 1;
+  const int NH = (int)(B >> lob);  // <= 256; the last partition also holds key B
   const uint32_t nblk = (uint32_t)nb(N);
   uint32_t* ptot = w.counts;           // NH partition totals
   uint32_t* hi_off = w.cursor;         // NH + 1
   uint32_t* bh = w.blockhist;          // NH x nblk
-  hipLaunchKernelGGL(k_sort_hist, dim3(nblk), dim3(256), 0, st, bh, scalars, N, c, W, lob, NH, nblk);
-  hipLaunchKernelGGL(k_sort_scan_blocks, dim3(NH), dim3(256), 0, st, bh, ptot, nblk);
-  hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(64), 0, st, hi_off, ptot, NH, w.offsets, B);
-  hipLaunchKernelGGL(k_sort_part, dim3(nblk), dim3(256), 0, st, (uint32_t*)w.digit, w.lo, bh, hi_off, scalars, N,
-                     tb.npts, c, W, lob, NH, nblk);
-  hipLaunchKernelGGL(k_sort_lo, dim3(NH), dim3(1024), 0, st, w.sorted, w.offsets, (const uint32_t*)w.digit, w.lo,
-                     hi_off, lob, B);
+  const size_t part_lds = (size_t)256 * W * 6;
+  switch (c) {
+#define KGS_SORT_C(CC)                                                                                         \
+  case CC:                                                                                                      \
+    hipLaunchKernelGGL(k_sort_hist<CC>, dim3(nblk), dim3(256), 0, st, bh, scalars, N, lob, NH, nblk);         \
+    hipLaunchKernelGGL(k_sort_scan_blocks, dim3(NH), dim3(256), 0, st, bh, ptot, nblk);                       \
+    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(64), 0, st, hi_off, ptot, NH, w.offsets, B);               \
+    hipLaunchKernelGGL(k_sort_part<CC>, dim3(nblk), dim3(256), part_lds, st, (uint32_t*)w.digit, w.lo, bh,   \
+                       ptot, hi_off, scalars, N, tb.npts, lob, NH, nblk);                                     \
+    break;
+    KGS_SORT_C(7) KGS_SORT_C(8) KGS_SORT_C(9) KGS_SORT_C(10) KGS_SORT_C(11) KGS_SORT_C(12)
+    KGS_SORT_C(13) KGS_SORT_C(14) KGS_SORT_C(15) KGS_SORT_C(16)
+#undef KGS_SORT_C
+    default:
+      return;  // choose_c keeps 7 <= c <= 16
+  }
+  hipLaunchKernelGGL(k_sort_lo, dim3(NH), dim3(SL_THREADS), 0, st, w.sorted, w.offsets, (const uint32_t*)w.digit,
+                     w.lo, hi_off, lob, NH, B);
   if (ev) hipEventRecord(ev[1], st);
   const uint64_t E = N * (uint64_t)W;  // upper bound of nonzero entries
   uint64_t L = E >> 18;
@@ -348,12 +490,12 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   hipLaunchKernelGGL(k_accumulate, dim3(nb(nseg)), dim3(256), 0, st, w.bstart, w.segpart, w.sorted, w.offsets,
                      B + 1, tb.table, (uint32_t)L);
   if (ev) hipEventRecord(ev[2], st);
-  hipLaunchKernelGGL(k_combine, dim3(nb(B)), dim3(256), 0, st, w.buckets, w.bstart, w.segpart, w.offsets, B,
+  hipLaunchKernelGGL(k_combine, dim3(nb(2 * (uint64_t)B)), dim3(256), 0, st, w.buckets, w.bstart, w.segpart, w.offsets, B,
                      (uint32_t)L);
   if (ev) hipEventRecord(ev[3], st);
-  const uint32_t chunks = (B / 2 + 255) / 256 > 0 ? (B / 2 + 255) / 256 : 1;
+  const uint32_t chunks = (B / 2 + BS_SPAN - 1) / BS_SPAN > 0 ? (B / 2 + BS_SPAN - 1) / BS_SPAN : 1;
   hipLaunchKernelGGL(k_bitsum1, dim3(chunks, c), dim3(256), 0, st, w.part, w.buckets, c, chunks);
-  hipLaunchKernelGGL(k_bitsum2, dim3(c), dim3(256), 0, st, T_out, w.part, chunks);
+  hipLaunchKernelGGL(k_bitsum2, dim3(c), dim3(64), 0, st, T_out, w.part, chunks);
   if (ev) hipEventRecord(ev[4], st);
 }
 

@@ -260,7 +260,7 @@ int choose_c(uint64_t npts) {
   int lg = 0;
   while ((1ull << lg) < npts) lg++;
   int cc = lg - 4;
-  if (cc < 6) cc = 6;
+  if (cc < 7) cc = 7;  // staging LDS of the partition pass: 256 * ceil(255/c) * 6 B <= 57 KB
   if (cc > 16) cc = 16;
   return cc;
 }
