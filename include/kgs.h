@@ -114,6 +114,17 @@ int kgs_prove_device(kgs_ctx_t* ctx, int kind, int nbits, int npols, const void*
 /* number of commitments / evaluations a proof of this shape produces */
 int kgs_proof_shape(int kind, int npols, int selected, int* n_commitments, int* n_evaluations);
 
+/* ---- verifiers (host only; no context, no GPU) -------------------------------------------
+ * mset_eq_kzg_grandsum_verifier / mset_eq_kzg_grandproduct_verifier
+ * (src/grandsum/mset_eq_kzg_verifier.js:9, src/grandproduct/mset_eq_kzg_verifier.js:9): commitment
+ * and evaluation buffers in the fixed order kgs_prove writes (kgs_proof_shape); tau_g2 = [tau]_2 as
+ * 128 B LEM (the second point of ptau section 3, kgs_ptau_read_tau_g2). Returns 1 (valid), 0
+ * (invalid: not on G1, evaluation >= r, or the pairing equation fails) or a negative error. */
+int kgs_verify(int kind, int nbits, int npols, int selected, const uint8_t* commitments, const uint8_t* evaluations,
+               const uint8_t tau_g2[128]);
+int kgs_verify_ptau(int kind, const char* ptau_path, int nbits, int npols, int selected, const uint8_t* commitments,
+                    const uint8_t* evaluations);
+
 /* Per-proof timing of the last kgs_prove* call (milliseconds, host wall clock per round). */
 int kgs_last_timing(kgs_ctx_t* ctx, double* rounds_ms, int max_rounds);
 

@@ -77,6 +77,9 @@ def lib():
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
         L.kgs_bench_ntt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_double)]
+        L.kgs_verify.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_u8p, c_u8p, c_u8p]
+        L.kgs_verify_ptau.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_u8p,
+                                      c_u8p]
         L.kgs_ctx_set_shard.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.kgs_shard_range.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_uint64)]
@@ -420,3 +423,35 @@ def grandproduct_prover(pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSel
         return _prover(GRANDPRODUCT, pTauFilename, evalsFs, evalsTs, evalsSelF, evalsSelT, device)
     except KgsError as e:
         raise ValueError(str(e)) from e
+
+
+def _verifier(kind, pTauFilename, proof, nBits):
+    """src/{grandsum,grandproduct}/mset_eq_kzg_verifier.js:9 — the proof's shape is read from its
+    keys as the reference does (nPols from /^F[0-9]/, selectors from /^selF/); the check runs in
+    libkgs (kgs_verify_ptau: transcript replay + optimal-ate pairing, host only)."""
+    import re
+    keys = list(proof["commitments"].keys())
+    nfi = len([k for k in keys if re.match(r"^F\d", k)])
+    npols = nfi if nfi > 0 else 1
+    selected = len([k for k in keys if re.match(r"^selF", k)]) == 1
+    cn, en = proof_names(kind, npols, selected)
+    try:
+        com = b"".join(bytes(proof["commitments"][n]) for n in cn)
+        ev = b"".join(bytes(proof["evaluations"][n]) for n in en)
+    except KeyError:
+        return False
+    if len(com) != 64 * len(cn) or len(ev) != 32 * len(en):
+        return False
+    rc = _check(lib().kgs_verify_ptau(kind, os.fsencode(pTauFilename), nBits, npols, 1 if selected else 0,
+                                      _buf(com), _buf(ev)))
+    return rc == 1
+
+
+def grandsum_verifier(pTauFilename, proof, nBits):
+    """mset_eq_kzg_grandsum_verifier (src/grandsum/mset_eq_kzg_verifier.js:9)."""
+    return _verifier(GRANDSUM, pTauFilename, proof, nBits)
+
+
+def grandproduct_verifier(pTauFilename, proof, nBits):
+    """mset_eq_kzg_grandproduct_verifier (src/grandproduct/mset_eq_kzg_verifier.js:9)."""
+    return _verifier(GRANDPRODUCT, pTauFilename, proof, nBits)

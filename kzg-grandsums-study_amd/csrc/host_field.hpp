@@ -18,12 +18,12 @@ struct Mod {
   uint64_t r2[4];
 };
 
-static const Mod FQ_MOD = {
+inline constexpr Mod FQ_MOD = {
     {0x3c208c16d87cfd47ull, 0x97816a916871ca8dull, 0xb85045b68181585dull, 0x30644e72e131a029ull},
     0x87d20782e4866389ull,
     {0xd35d438dc58f0d9dull, 0x0a78eb28f5c70b3dull, 0x666ea36f7879462cull, 0x0e0a77c19a07df2full},
     {0xf32cfc5b538afa89ull, 0xb5e71911d44501fbull, 0x47ab1eff0a417ff6ull, 0x06d89f71cab8351full}};
-static const Mod FR_MOD = {
+inline constexpr Mod FR_MOD = {
     {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull, 0x30644e72e131a029ull},
     0xc2e1f593efffffffull,
     {0xac96341c4ffffffbull, 0x36fc76959f60cd29ull, 0x666ea36f7879462eull, 0x0e0a77c19a07df2full},
@@ -85,6 +85,7 @@ struct F {
     return r;
   }
   F neg() const { return is_zero() ? *this : zero() - *this; }
+  F dbl() const { return *this + *this; }
   friend F operator*(const F& a, const F& b) {
     uint64_t t[6] = {0, 0, 0, 0, 0, 0};
     for (int i = 0; i < 4; i++) {
@@ -166,6 +167,23 @@ struct F {
 
 typedef F<FR_MOD> Fr;
 typedef F<FQ_MOD> Fq;
+
+// Fr.w[k] (standard BN254 roots: nqr = 5, s = 28) and the coset shift g = 5
+inline Fr fr_w(int k) {
+  // (r-1) >> 28
+  uint64_t e[4];
+  memcpy(e, host::FR_MOD.p, 32);
+  e[0] -= 1;
+  for (int s = 0; s < 28; s++) {
+    e[0] = (e[0] >> 1) | (e[1] << 63);
+    e[1] = (e[1] >> 1) | (e[2] << 63);
+    e[2] = (e[2] >> 1) | (e[3] << 63);
+    e[3] >>= 1;
+  }
+  Fr w = Fr::from_u64(5).pow(e);
+  for (int s = 28; s > k; s--) w = w.sqr();
+  return w;
+}
 
 // G1 in XYZZ on the host (matches the device layout: X,Y,ZZ,ZZZ, 128 B)
 struct G1 {

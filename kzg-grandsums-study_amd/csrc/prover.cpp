@@ -25,8 +25,10 @@
 
 #include "../../include/kgs.h"
 #include "host_field.hpp"
+#include "host_pairing.hpp"
 #include "kernels.hpp"
 #include "keccak.hpp"
+#include "transcript.hpp"
 
 using namespace kgs;
 using host::Fq;
@@ -53,47 +55,13 @@ static void check_launch() {
   if (e != hipSuccess) throw KgsError(KGS_E_HIP, std::string("HIP launch error: ") + hipGetErrorString(e));
 }
 
-// ------------------------------------------------------------------ constants
-// Fr.w[k] (standard BN254 roots: nqr = 5, s = 28) and the coset shift g = 5
-static Fr fr_w(int k) {
-  // (r-1) >> 28
-  uint64_t e[4];
-  memcpy(e, host::FR_MOD.p, 32);
-  e[0] -= 1;
-  for (int s = 0; s < 28; s++) {
-    e[0] = (e[0] >> 1) | (e[1] << 63);
-    e[1] = (e[1] >> 1) | (e[2] << 63);
-    e[2] = (e[2] >> 1) | (e[3] << 63);
-    e[3] >>= 1;
-  }
-  Fr w = Fr::from_u64(5).pow(e);
-  for (int s = 28; s > k; s--) w = w.sqr();
-  return w;
-}
+using host::fr_w;
 
 struct DBuf {
   void* p = nullptr;
   size_t bytes = 0;
 };
 
-struct Transcript {
-  std::vector<uint8_t> buf;
-  void add_commitment(const uint8_t lem[64]) {
-    uint8_t rpr[64];
-    host::g1_lem_to_rpr_uncompressed(lem, rpr);
-    buf.insert(buf.end(), rpr, rpr + 64);
-  }
-  void add_scalar(const Fr& s) {
-    uint8_t be[32];
-    s.to_be_std(be);
-    buf.insert(buf.end(), be, be + 32);
-  }
-  Fr challenge() const {
-    uint8_t h[32];
-    host::keccak256(buf.data(), buf.size(), h);
-    return Fr::from_be_reduce(h);
-  }
-};
 
 }  // namespace
 
@@ -525,7 +493,7 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   lap(0);
 
   // ---------------- round 2: challenges, combined polynomials, S / Z (prover.js:181-231)
-  Transcript tr;
+  host::Transcript tr;
   for (int i = 0; i < ci; i++) tr.add_commitment(com[i].data());
   Fr beta = Fr::zero();
   if (vec) {
@@ -821,64 +789,12 @@ PtauInfo read_ptau_header(FILE* f, const char* path) {
   return info;
 }
 
-// ------------------------------------------------------------------ host G2 (synthetic ptau)
-struct Fq2 {
-  Fq a, b;  // a + b u, u^2 = -1
-  Fq2 operator+(const Fq2& o) const { return {a + o.a, b + o.b}; }
-  Fq2 operator-(const Fq2& o) const { return {a - o.a, b - o.b}; }
-  Fq2 operator*(const Fq2& o) const { return {a * o.a - b * o.b, a * o.b + b * o.a}; }
-  Fq2 inv() const {
-    Fq d = (a.sqr() + b.sqr()).inverse();
-    return {a * d, b.neg() * d};
-  }
-  bool is_zero() const { return a.is_zero() && b.is_zero(); }
-  bool operator==(const Fq2& o) const { return a == o.a && b == o.b; }
-};
-struct G2A {
-  Fq2 x, y;
-  bool inf;
-};
-G2A g2_add(const G2A& p, const G2A& q) {
-  if (p.inf) return q;
-  if (q.inf) return p;
-  Fq2 lam;
-  if (p.x == q.x) {
-    if ((p.y + q.y).is_zero()) return {p.x, p.y, true};
-    Fq2 x2 = p.x * p.x;
-    lam = (x2 + x2 + x2) * (p.y + p.y).inv();
-  } else {
-    lam = (q.y - p.y) * (q.x - p.x).inv();
-  }
-  G2A r;
-  r.inf = false;
-  r.x = lam * lam - p.x - q.x;
-  r.y = lam * (p.x - r.x) - p.y;
-  return r;
-}
-Fq fq_from_dec(const char* s) {
-  Fq acc = Fq::zero(), ten = Fq::from_u64(10);
-  for (; *s; s++) acc = acc * ten + Fq::from_u64((uint64_t)(*s - '0'));
-  return acc;
-}
-G2A g2_gen() {
-  G2A g;
-  g.inf = false;
-  g.x = {fq_from_dec("10857046999023057135944570762232829481370756359578518086990519993285655852781"),
-         fq_from_dec("11559732032986387107991004021392285783925812861821192530917403151452391805634")};
-  g.y = {fq_from_dec("8495653923123431417604973247489272438418190587263600148770280649306958101930"),
-         fq_from_dec("4082367875863433681332203403145435568316851327593401208105741076214120093531")};
-  return g;
-}
-void g2_lem(const G2A& p, uint8_t out[128]) {
-  if (p.inf) {
-    memset(out, 0, 128);
-    return;
-  }
-  p.x.a.to_bytes(out);
-  p.x.b.to_bytes(out + 32);
-  p.y.a.to_bytes(out + 64);
-  p.y.b.to_bytes(out + 96);
-}
+// ------------------------------------------------------------------ host G2 (synthetic ptau): host_pairing.hpp
+using host::Fq2;
+using host::G2A;
+using host::g2_add;
+using host::g2_gen;
+using host::g2_lem;
 
 // fixed-base table (d * 2^(8j)) G, affine LEM, 32 x 256
 std::vector<uint8_t> g1_fixed_table() {

@@ -244,6 +244,40 @@ static napi_value Prove(napi_env env, napi_callback_info info) {
   return queue(env, j, "kgs_prove");
 }
 
+// verifyPtau(kind, ptauPath, nbits, npols, selected, commitments(Uint8Array), evaluations(Uint8Array))
+// -> boolean (host-only pairing check, kgs_verify_ptau)
+static napi_value VerifyPtau(napi_env env, napi_callback_info info) {
+  size_t argc = 7;
+  napi_value argv[7];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  int32_t kind = 0, nbits = 0, npols = 0;
+  bool selected = false;
+  napi_get_value_int32(env, argv[0], &kind);
+  size_t plen = 0;
+  napi_get_value_string_utf8(env, argv[1], nullptr, 0, &plen);
+  std::string path(plen + 1, '\0');
+  napi_get_value_string_utf8(env, argv[1], &path[0], plen + 1, &plen);
+  path.resize(plen);
+  napi_get_value_int32(env, argv[2], &nbits);
+  napi_get_value_int32(env, argv[3], &npols);
+  napi_get_value_bool(env, argv[4], &selected);
+  std::vector<uint8_t> com = bytes_of(env, argv[5]), ev = bytes_of(env, argv[6]);
+  int nc = 0, ne = 0;
+  kgs_proof_shape(kind, npols, selected ? 1 : 0, &nc, &ne);
+  if (com.size() != (size_t)nc * 64 || ev.size() != (size_t)ne * 32) {
+    napi_throw_error(env, nullptr, "proof buffers do not match the proof shape");
+    return nullptr;
+  }
+  int rc = kgs_verify_ptau(kind, path.c_str(), nbits, npols, selected ? 1 : 0, com.data(), ev.data());
+  if (rc < 0) {
+    napi_throw_error(env, nullptr, "kgs_verify_ptau failed");
+    return nullptr;
+  }
+  napi_value out;
+  napi_get_boolean(env, rc == 1, &out);
+  return out;
+}
+
 static napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor desc[] = {
       {"ctxCreate", nullptr, CtxCreate, nullptr, nullptr, nullptr, napi_default, nullptr},
@@ -251,6 +285,7 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"srsInfo", nullptr, SrsInfo, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"prove", nullptr, Prove, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"keccak256", nullptr, Keccak, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"verifyPtau", nullptr, VerifyPtau, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(desc) / sizeof(desc[0]), desc);
   return exports;

@@ -4,4 +4,6 @@ module.exports = {
     Evaluations: require("./src/polynomial/evaluations").Evaluations,
     mset_eq_kzg_grandsum_prover: require("./src/grandsum/mset_eq_kzg_prover"),
     mset_eq_kzg_grandproduct_prover: require("./src/grandproduct/mset_eq_kzg_prover"),
+    mset_eq_kzg_grandsum_verifier: require("./src/grandsum/mset_eq_kzg_verifier"),
+    mset_eq_kzg_grandproduct_verifier: require("./src/grandproduct/mset_eq_kzg_verifier"),
 };

@@ -223,6 +223,9 @@ def test_large_proof_properties(K, kind, nbits, npols, sel):
     proof = {"commitments": dict(zip(cn, coms)), "evaluations": dict(zip(en, evs))}
     from oracle.ptau import PTau
     assert P.verify(kind, PTau(path), proof, nbits, tau=common.tau())
+    # and with the native pairing verifier (kgs_verify_ptau), as the reference's verifier module does
+    vf = K.grandsum_verifier if kind == "grandsum" else K.grandproduct_verifier
+    assert vf(path, proof, nbits) is True
     # transcript-independent commitment: C(F0) == F0(tau) G1
     ftau = _bary_eval(fvals[0], nbits, common.tau())
     assert proof["commitments"]["F0" if npols > 1 else "F"] == bn.g1_to_lem(bn.g1_mul(bn.G1_GEN, ftau))
