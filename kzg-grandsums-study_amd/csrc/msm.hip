@@ -76,8 +76,8 @@ void msm_build_table(hipStream_t st, uint32_t* table, uint64_t npts, int c, int 
 // ------------------------------------------------------------------ digits + two-pass bucket sort
 // Entry (j, i) = (window, point) with signed digit d = digit_j(from_mont(scalar_i)); key |d| in
 // [0, B], B = 2^(c-1); key 0 entries are dropped. Sort by key without global per-entry atomics:
-//  pass 1 partitions by p = min(key >> LOB, NH - 1) (NH = B >> LOB <= 256 partitions; the last
-//          one also holds key B). Per-block partition counts come from a histogram pass whose
+//  sorting is by k' = key - 1 in [0, B) (c - 1 bits): pass 1 partitions by p = k' >> LOB
+//          (NH = B >> LOB <= 256 partitions of 2^LOB keys each). Per-block partition counts come from a histogram pass whose
 //          block x partition table is scanned; each block then counting-sorts its entries in LDS
 //          and writes them out as contiguous per-partition runs (coalesced stores instead of one
 //          scattered 4 B + 1 B store per entry). Digits are RECOMPUTED from the scalars in both
@@ -130,10 +130,8 @@ __device__ __forceinline__ uint32_t wave_excl_scan256(const uint32_t* a, uint32_
   return __shfl(incl, 63);  // total
 }
 
-__device__ __forceinline__ uint32_t part_of(uint32_t key, int lob, int NH) {
-  const uint32_t p = key >> lob;
-  return p < (uint32_t)NH ? p : (uint32_t)NH - 1;
-}
+// partition of a nonzero digit magnitude: (key - 1) >> lob
+__device__ __forceinline__ uint32_t part_of(uint32_t key, int lob) { return (key - 1) >> lob; }
 
 template <int C>
 __global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ bh, const uint32_t* __restrict__ sc,
@@ -149,7 +147,7 @@ __global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ bh, co
     scalar_digits<C>(d, sc, i);
 #pragma unroll
     for (int j = 0; j < W; j++) {
-      if (d[j]) atomicAdd(&h[part_of((uint32_t)(d[j] < 0 ? -d[j] : d[j]), lob, NH)], 1u);
+      if (d[j]) atomicAdd(&h[part_of((uint32_t)(d[j] < 0 ? -d[j] : d[j]), lob)], 1u);
     }
   }
   __syncthreads();
@@ -188,6 +186,7 @@ __global__ void __launch_bounds__(64) k_sort_scan(uint32_t* __restrict__ hi_off,
   const uint32_t total = wave_excl_scan256(ptot, hi_off, NH);
   if (threadIdx.x == 0) {
     hi_off[NH] = total;
+    offsets[0] = 0;  // key 0 (zero digits) is never stored
     offsets[B + 1] = total;
   }
 }
@@ -201,7 +200,7 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
   constexpr int W = (255 + C - 1) / C;
   extern __shared__ uint32_t smem[];
   uint32_t* sval = smem;                             // 256 * W
-  uint16_t* skey = (uint16_t*)(smem + 256 * W);      // 256 * W (key <= 2^15)
+  uint16_t* skey = (uint16_t*)(smem + 256 * W);      // 256 * W (key - 1 < 2^16)
   __shared__ uint32_t base[256], loff[256], cur[256];
   __shared__ uint32_t total;
   const uint32_t blk = blockIdx.x, tid = threadIdx.x;
@@ -227,16 +226,16 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
     for (int j = 0; j < W; j++) {
       if (!d[j]) continue;
       const uint32_t k = (uint32_t)(d[j] < 0 ? -d[j] : d[j]);
-      const uint32_t pos = atomicAdd(&cur[part_of(k, lob, NH)], 1u);
+      const uint32_t pos = atomicAdd(&cur[part_of(k, lob)], 1u);
       sval[pos] = (uint32_t)((uint64_t)j * Nsrs + i) | (d[j] < 0 ? 0x80000000u : 0u);
-      skey[pos] = (uint16_t)k;
+      skey[pos] = (uint16_t)(k - 1);
     }
   }
   __syncthreads();
   const uint32_t tot = total;
   for (uint32_t e = tid; e < tot; e += 256) {
-    const uint32_t k = skey[e];
-    const uint32_t p = part_of(k, lob, NH);
+    const uint32_t k = skey[e];  // key - 1
+    const uint32_t p = k >> lob;
     const uint32_t g = base[p] + (e - loff[p]);
     tval[g] = sval[e];
     tlo[g] = (uint8_t)(k - (p << lob));
@@ -257,7 +256,7 @@ __global__ void __launch_bounds__(SL_THREADS) k_sort_lo(uint32_t* __restrict__ s
   __shared__ uint8_t sl[SL_TILE];
   const int p = blockIdx.x;
   const uint32_t tid = threadIdx.x;
-  const int nb = (1 << lob) + (p == NH - 1 ? 1 : 0);  // the last partition also holds key B
+  const int nb = 1 << lob;  // keys (p << lob) + 1 .. ((p + 1) << lob)
   const uint32_t s0 = hi_off[p], s1 = hi_off[p + 1];
   if ((int)tid < nb) cnt[tid] = 0;
   __syncthreads();
@@ -267,8 +266,7 @@ __global__ void __launch_bounds__(SL_THREADS) k_sort_lo(uint32_t* __restrict__ s
     wave_excl_scan256(cnt, cur, nb);
     for (int b = tid; b < nb; b += 64) {
       cur[b] += s0;
-      const uint32_t key = ((uint32_t)p << lob) + b;
-      if (key <= B) offsets[key] = cur[b];
+      offsets[((uint32_t)p << lob) + b + 1] = cur[b];
     }
   }
   __syncthreads();
@@ -457,8 +455,11 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   if (ev) hipEventRecord(ev[0], st);
   const int c = tb.c, W = tb.W;
   const uint32_t B = 1u << (c - 1);
-  const int lob = c - 1 < 7 ? c - 1 : 7;
-  const int NH = (int)(B >> lob);  // <= 256; the last partition also holds key B
+  // LOB bits of (key - 1) are sorted inside a partition (<= 8: tlo is a byte), the rest select one
+  // of NH = B >> LOB <= 256 partitions
+  int lob = c - 1 < 7 ? c - 1 : 7;
+  if (c - 9 > lob) lob = c - 9;
+  const int NH = (int)(B >> lob);
   const uint32_t nblk = (uint32_t)nb(N);
   uint32_t* ptot = w.counts;           // NH partition totals
   uint32_t* hi_off = w.cursor;         // NH + 1
@@ -474,10 +475,10 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
                        ptot, hi_off, scalars, N, tb.npts, lob, NH, nblk);                                     \
     break;
     KGS_SORT_C(7) KGS_SORT_C(8) KGS_SORT_C(9) KGS_SORT_C(10) KGS_SORT_C(11) KGS_SORT_C(12)
-    KGS_SORT_C(13) KGS_SORT_C(14) KGS_SORT_C(15) KGS_SORT_C(16)
+    KGS_SORT_C(13) KGS_SORT_C(14) KGS_SORT_C(15) KGS_SORT_C(16) KGS_SORT_C(17)
 #undef KGS_SORT_C
     default:
-      return;  // choose_c keeps 7 <= c <= 16
+      return;  // choose_c keeps 7 <= c <= 17
   }
   hipLaunchKernelGGL(k_sort_lo, dim3(NH), dim3(SL_THREADS), 0, st, w.sorted, w.offsets, (const uint32_t*)w.digit,
                      w.lo, hi_off, lob, NH, B);

@@ -15,6 +15,7 @@
 //  * commitments skip zero top coefficients by degree bounds (zero scalars add nothing).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <chrono>
 #include <map>
@@ -56,6 +57,10 @@ static void check_launch() {
 }
 
 using host::fr_w;
+
+#ifndef KGS_C_MAX
+#define KGS_C_MAX 17
+#endif
 
 struct DBuf {
   void* p = nullptr;
@@ -229,7 +234,11 @@ int choose_c(uint64_t npts) {
   while ((1ull << lg) < npts) lg++;
   int cc = lg - 4;
   if (cc < 7) cc = 7;  // staging LDS of the partition pass: 256 * ceil(255/c) * 6 B <= 57 KB
-  if (cc > 16) cc = 16;
+  if (cc > KGS_C_MAX) cc = KGS_C_MAX;
+  if (const char* e = getenv("KGS_MSM_C")) {  // A/B override of the window
+    int v = atoi(e);
+    if (v >= 7 && v <= 17) cc = v;
+  }
   return cc;
 }
 
