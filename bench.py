@@ -64,6 +64,79 @@ def bench_tau():
     return int.from_bytes(K.keccak256(b"kgs-bench-tau"), "big") % R
 
 
+# Collectives run on RCCL ("nccl") with device tensors. KGS_BENCH_BACKEND=gloo rehearses N > 1 on a
+# single-GPU box (host-tensor collectives, every rank on cuda:0); the driver never sets it.
+BACKEND = os.environ.get("KGS_BENCH_BACKEND", "nccl")
+
+
+def coll_device():
+    import torch
+    return "cpu" if BACKEND == "gloo" else f"cuda:{torch.cuda.current_device()}"
+
+
+def max_over_ranks(t):
+    import torch
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized():
+        return t
+    te = torch.tensor([t], dtype=torch.float64, device=coll_device())
+    dist.all_reduce(te, op=dist.ReduceOp.MAX)
+    return float(te.item())
+
+
+def selected_vector_leg(K, torch, dist, rank, world, local, args):
+    """BASELINE configs[4] / SURVEY C5: selected-vector grand-sum, k = 4, n = 2^22 (selF = ones but
+    the last, selT = ones but the first, T = rot(F)); same inputs on every rank. N > 1: MSMs
+    point-range sharded over all ranks (kgs_ctx_set_shard over torch.distributed = RCCL)."""
+    nb, k = args.sv_nbits, 4
+    n = 1 << nb
+    ctx = K.Context(local)
+    ptau = f"/tmp/kgs_bench_p{nb}_r{rank}.ptau"
+    t0 = time.time()
+    if not os.path.exists(ptau):
+        ctx.write_synthetic_ptau(ptau, nb, bench_tau())
+    ctx.load_ptau(ptau, nb)
+    setup_s = time.time() - t0
+    keep, d_f, d_t = [], [], []
+    for i in range(k):
+        f, t = synth_evals(n, 5000 + i)
+        tf = torch.from_numpy(f.reshape(-1).copy()).to(f"cuda:{local}")
+        tt = torch.from_numpy(t.reshape(-1).copy()).to(f"cuda:{local}")
+        keep += [tf, tt]
+        d_f.append(tf.data_ptr())
+        d_t.append(tt.data_ptr())
+    one = np.frombuffer(K.FR_ONE_MONT, dtype=np.uint8)
+    sf = np.tile(one, n)
+    st = sf.copy()
+    sf[32 * (n - 1):] = 0
+    st[:32] = 0
+    tsf = torch.from_numpy(sf).to(f"cuda:{local}")
+    tst = torch.from_numpy(st).to(f"cuda:{local}")
+    if world > 1:
+        ctx.set_shard(rank, world, K.torch_allgather(device=None if BACKEND == "gloo" else f"cuda:{local}"))
+    ctx.prove_device(K.GRANDSUM, nb, d_f, d_t, tsf.data_ptr(), tst.data_ptr())  # warm-up
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.sv_proofs):
+        coms = ctx.prove_device(K.GRANDSUM, nb, d_f, d_t, tsf.data_ptr(), tst.data_ptr())[0]
+    torch.cuda.synchronize()
+    el = max_over_ranks(time.perf_counter() - t1)
+    out = {"workload": f"selected-vector grand-sum, n=2^{nb}, k={k}, selectors", "n_gpus": world,
+           "mode": "msm point-range sharded (strong scaling)" if world > 1 else "single GPU",
+           "proofs": args.sv_proofs, "ms_per_proof": round(1000.0 * el / args.sv_proofs, 3),
+           "proofs_per_s": round(args.sv_proofs / el, 4), "srs_setup_s": round(setup_s, 2)}
+    if dist:
+        h = torch.tensor(list(K.keccak256(b"".join(coms))[:8]), dtype=torch.int64, device=coll_device())
+        hs = [torch.empty_like(h) for _ in range(world)]
+        dist.all_gather(hs, h)
+        out["ranks_agree"] = all(bool(torch.equal(hs[0], x)) for x in hs)
+    ctx.set_shard(0, 1)
+    ctx.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -75,9 +148,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--msm-reps", type=int, default=5)
-    ap.add_argument("--shard-proofs", type=int, default=3,
-                    help="N > 1: also time this many proofs with every MSM point-range sharded over all ranks "
-                         "(RCCL all-gather of the partials; 0 = skip)")
+    ap.add_argument("--no-extra-legs", dest="extra_legs", action="store_false",
+                    help="skip the grand-product (configs[2]) and selected-vector 2^22 (configs[4]) legs")
+    ap.add_argument("--sv-nbits", type=int, default=22)
+    ap.add_argument("--sv-proofs", type=int, default=3,
+                    help="proofs timed in the selected-vector leg (N > 1: MSMs sharded over all ranks)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="independent proofs in flight per GPU (one context + HIP stream + host thread each)")
     args = ap.parse_args()
@@ -90,7 +165,9 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        dist.init_process_group(BACKEND, rank=rank, world_size=world)
+        if BACKEND == "gloo":
+            local = 0
     torch.cuda.set_device(local)
     K = load_pkg()
     ctx = K.Context(local)
@@ -162,47 +239,35 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - ts
-    if dist:
-        te = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(te, op=dist.ReduceOp.MAX)
-        elapsed = float(te.item())
+    elapsed = max_over_ranks(elapsed)
     total_proofs = args.steps * world
     value = total_proofs / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
-    # ---------------- sharded leg (N > 1): one proof at a time over all GPUs, MSMs point-range
-    # sharded, NTT/elementwise work replicated; same inputs on every rank
-    sharded = None
-    if dist and args.shard_proofs > 0:
-        d_f = bufs[0][0]
-        d_t = bufs[0][1]
-        for i in range(args.npols):
-            keep[2 * i].copy_(torch.from_numpy(synth_evals(n, 4242 + i)[0].reshape(-1).copy()))
-            keep[2 * i + 1].copy_(torch.from_numpy(synth_evals(n, 4242 + i)[1].reshape(-1).copy()))
-        torch.cuda.synchronize()
-        ctx.set_shard(rank, world, K.torch_allgather(device=f"cuda:{local}"))
-        ctx.prove_device(kind, nbits, d_f, d_t)  # warm-up
-        dist.barrier()
+    # ---------------- extra configs (BASELINE.json configs[2] and [4]), outside the timed region
+    extra = {}
+    if args.extra_legs:
+        # C3: grand-product at the same n, same contexts / inputs (replicas per GPU)
+        gp_steps = 4 * len(ctxs)
+        kind_main = kind
+        kind = K.GRANDPRODUCT if kind_main == K.GRANDSUM else K.GRANDSUM
+        steps(len(ctxs))
+        if dist:
+            dist.barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        for _ in range(args.shard_proofs):
-            coms_sh = ctx.prove_device(kind, nbits, d_f, d_t)[0]
+        steps(gp_steps)
         torch.cuda.synchronize()
-        dist.barrier()
-        el = time.perf_counter() - t1
-        te = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(te, op=dist.ReduceOp.MAX)
-        el = float(te.item())
-        # all ranks must hold the same proof
-        h = torch.tensor(list(K.keccak256(b"".join(coms_sh))[:8]), dtype=torch.int64, device=f"cuda:{local}")
-        hs = [torch.empty_like(h) for _ in range(world)]
-        dist.all_gather(hs, h)
-        ctx.set_shard(0, 1)
-        sharded = {"n_gpus": world, "proofs": args.shard_proofs, "ms_per_proof": round(1000.0 * el / args.shard_proofs, 3),
-                   "proofs_per_s": round(args.shard_proofs / el, 4),
-                   "latency_speedup_vs_1gpu": round(latency_ms / (1000.0 * el / args.shard_proofs), 3),
-                   "ranks_agree": all(bool(torch.equal(hs[0], x)) for x in hs),
-                   "scaling": "strong (one proof split over all GPUs)"}
+        el = max_over_ranks(time.perf_counter() - t1)
+        extra["grandproduct_vs_grandsum" if kind_main == K.GRANDSUM else "grandsum_vs_grandproduct"] = {
+            "workload": f"{'grandproduct' if kind == K.GRANDPRODUCT else 'grandsum'} prover, n=2^{nbits}, k={args.npols}, no selectors",
+            "proofs_per_s": round(gp_steps * world / el, 4), "proofs": gp_steps * world}
+        kind = kind_main
+        # C5 (N = 1: one GPU; N > 1: every MSM point-range sharded over all ranks, RCCL all-gather)
+        for c in ctxs[1:]:
+            c.close()
+        ctxs[1:] = []
+        extra["selected_vector"] = selected_vector_leg(K, torch, dist, rank, world, local, args)
 
     if rank != 0:
         if dist:
@@ -255,6 +320,15 @@ def main():
                 "algorithmic_bytes_per_launch": 68 * entries.value,
                 "hbm_gbps_algorithmic": round(68 * entries.value / (acc_ms / 1e3) / 1e9, 1)}
 
+    # ---------------- proof-level HBM view (north star: achieved HBM-bandwidth fraction). Bytes per
+    # proof = SURVEY.md §8d's count over the REFERENCE op list, B_gs(n) = 131 E = 4192 n (grand-sum,
+    # k = 1, no selectors); the re-planned GPU path moves fewer, so this is an upper-bound view.
+    b_proof = (4192 if args.kind == "grandsum" else 101 * 32) * n
+    hbm_view = {"algorithmic_bytes_per_proof": b_proof, "achieved_GBps": round(b_proof * value / 1e9, 1),
+                "peak_GBps": 8000.0, "frac": round(b_proof * value / 1e9 / 8000.0, 4),
+                "accumulate_pmc_GBps": round(traffic / (acc_ms / 1e3) / 1e9, 1) if traffic else None,
+                "note": "the proof is INT-VALU bound (MSM bucket accumulation), not HBM bound"}
+
     # ---------------- CPU baseline (oracle/c port of the reference op list), N = 1 only
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -286,7 +360,8 @@ def main():
         "round_ms_single_proof": [round(x, 3) for x in rounds],
         "msm": msm,
         "roofline": roofline,
-        "sharded_msm": sharded,
+        "hbm_view": hbm_view,
+        "extra_configs": extra,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out))

@@ -36,6 +36,7 @@ struct MsmWork {
   uint32_t* blockhist = nullptr;  // (NH <= 264) x ceil(N/256) per-block partition counts
   uint32_t *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *sorted = nullptr;
   uint32_t *bstart = nullptr, *segpart = nullptr, *buckets = nullptr, *part = nullptr;
+  uint32_t* segowner = nullptr;  // bucket of each segment's first run
 };
 
 // ntt.hip

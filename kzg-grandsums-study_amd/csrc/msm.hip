@@ -325,6 +325,7 @@ __device__ __forceinline__ void emit_run(uint32_t* bstart, uint32_t* segpart, ui
 #define KGS_ACC_WAVES 1
 #endif
 __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __restrict__ bstart, uint32_t* __restrict__ segpart,
+                                                    uint32_t* __restrict__ segowner,
                                                     const uint32_t* __restrict__ sorted,
                                                     const uint32_t* __restrict__ offsets, uint32_t nbins,
                                                     const uint32_t* __restrict__ table, uint32_t L) {
@@ -340,6 +341,7 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
     if (offsets[mid] <= start) lo = mid; else hi = mid;
   }
   uint32_t b = lo;
+  segowner[s] = b;  // bucket of the segment's first run (read by the combine levels)
   uint64_t rs = start;
   uint64_t bend = offsets[b + 1];
   g1_xyzz acc = g1_xyzz::inf();
@@ -358,8 +360,17 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
   emit_run(bstart, segpart, b, rs, offsets, s, acc);
 }
 
-// bucket b = bstart[b] + the segment partials of the segments starting strictly inside it; two
-// lanes per bucket (even / odd segments), joined by one xor-shuffle add
+// Bucket totals. Bucket b = bstart[b] + the partials of the segments whose start lies strictly
+// inside it: segments s_lo(b) = offsets[b]/L + 1 .. s_hi(b) = ceil(offsets[b+1]/L) - 1. Buckets can be
+// arbitrarily skewed (a selector polynomial has all-equal coefficients, so every point lands in the
+// same bucket of each window), so the partials are first reduced in CB_LEVELS chunked levels: at
+// level j the thread of segment s = s_lo + i*CB_T^(j+1) adds the CB_T partials at stride CB_T^j that
+// follow it (in place). The final pass then has <= ceil(m / CB_T^CB_LEVELS) partials per bucket, two
+// lanes per bucket joined by one xor-shuffle add. Depth for m partials: ~CB_T*CB_LEVELS + m/CB_T^3.
+// Lists of <= CB_T partials (every bucket of a uniform scalar distribution) skip the levels.
+constexpr uint32_t CB_T = 16;
+constexpr int CB_LEVELS = 3;
+
 __device__ __forceinline__ g1_xyzz shfl_xor_pt(const g1_xyzz& a, int mask) {
   g1_xyzz r;
 #pragma unroll
@@ -372,9 +383,30 @@ __device__ __forceinline__ g1_xyzz shfl_xor_pt(const g1_xyzz& a, int mask) {
   return r;
 }
 
+__global__ void __launch_bounds__(256) k_combine_level(uint32_t* __restrict__ segpart,
+                                                       const uint32_t* __restrict__ segowner,
+                                                       const uint32_t* __restrict__ offsets, uint32_t nbins,
+                                                       uint32_t L, uint64_t stride) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t E = offsets[nbins];
+  if (s * L >= E) return;
+  const uint32_t b = segowner[s];
+  const uint64_t o0 = offsets[b], o1 = offsets[b + 1];
+  if (s * L <= o0) return;  // this segment's first run starts its bucket (bstart), not a partial
+  const uint64_t s_lo = o0 / L + 1, s_hi = (o1 + L - 1) / L;  // partials [s_lo, s_hi)
+  if (s_hi - s_lo <= CB_T) return;  // short lists are summed directly by k_combine
+  if ((s - s_lo) % (stride * CB_T) != 0) return;
+  const uint64_t top = s + stride * CB_T < s_hi ? s + stride * CB_T : s_hi;
+  if (s + stride >= top) return;  // nothing to add
+  g1_xyzz acc = g1_xyzz::load(segpart + 32 * s);
+  for (uint64_t t = s + stride; t < top; t += stride) acc.add(g1_xyzz::load(segpart + 32 * t));
+  acc.store(segpart + 32 * s);
+}
+
 __global__ void __launch_bounds__(256) k_combine(uint32_t* __restrict__ buckets, const uint32_t* __restrict__ bstart,
                                                  const uint32_t* __restrict__ segpart,
-                                                 const uint32_t* __restrict__ offsets, uint32_t B, uint32_t L) {
+                                                 const uint32_t* __restrict__ offsets, uint32_t B, uint32_t L,
+                                                 uint64_t stride) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t b = (g >> 1) + 1;  // buckets 1..B
   const uint32_t sub = g & 1;
@@ -383,7 +415,9 @@ __global__ void __launch_bounds__(256) k_combine(uint32_t* __restrict__ buckets,
     const uint64_t o0 = offsets[b], o1 = offsets[b + 1];
     if (o1 > o0) {
       if (sub == 0) acc = g1_xyzz::load(bstart + 32 * (uint64_t)b);
-      for (uint64_t sgm = o0 / L + 1 + sub; sgm * L < o1; sgm += 2) acc.add(g1_xyzz::load(segpart + 32 * sgm));
+      const uint64_t s_lo = o0 / L + 1, s_hi = (o1 + L - 1) / L;
+      const uint64_t st = s_hi > s_lo + CB_T ? stride : 1;  // reduced by the levels, or short
+      for (uint64_t sgm = s_lo + sub * st; sgm < s_hi; sgm += 2 * st) acc.add(g1_xyzz::load(segpart + 32 * sgm));
     }
   }
   acc.add(shfl_xor_pt(acc, 1));
@@ -488,11 +522,15 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   if (L < 4) L = 4;
   if (L > 64) L = 64;
   const uint64_t nseg = (E + L - 1) / L;
-  hipLaunchKernelGGL(k_accumulate, dim3(nb(nseg)), dim3(256), 0, st, w.bstart, w.segpart, w.sorted, w.offsets,
-                     B + 1, tb.table, (uint32_t)L);
+  hipLaunchKernelGGL(k_accumulate, dim3(nb(nseg)), dim3(256), 0, st, w.bstart, w.segpart, w.segowner, w.sorted,
+                     w.offsets, B + 1, tb.table, (uint32_t)L);
   if (ev) hipEventRecord(ev[2], st);
-  hipLaunchKernelGGL(k_combine, dim3(nb(2 * (uint64_t)B)), dim3(256), 0, st, w.buckets, w.bstart, w.segpart, w.offsets, B,
-                     (uint32_t)L);
+  uint64_t stride = 1;
+  for (int j = 0; j < CB_LEVELS; j++, stride *= CB_T)
+    hipLaunchKernelGGL(k_combine_level, dim3(nb(nseg)), dim3(256), 0, st, w.segpart, w.segowner, w.offsets, B + 1,
+                       (uint32_t)L, stride);
+  hipLaunchKernelGGL(k_combine, dim3(nb(2 * (uint64_t)B)), dim3(256), 0, st, w.buckets, w.bstart, w.segpart,
+                     w.offsets, B, (uint32_t)L, stride);
   if (ev) hipEventRecord(ev[3], st);
   const uint32_t chunks = (B / 2 + BS_SPAN - 1) / BS_SPAN > 0 ? (B / 2 + BS_SPAN - 1) / BS_SPAN : 1;
   hipLaunchKernelGGL(k_bitsum1, dim3(chunks, c), dim3(256), 0, st, w.part, w.buckets, c, chunks);

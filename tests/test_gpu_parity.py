@@ -77,6 +77,32 @@ def test_msm(ctx9):
     assert ctx9.msm(common.mont_bytes([0] * 8)) == bytes(64)  # infinity
 
 
+def test_msm_skewed_buckets(K):
+    """Repeated scalars pile every point into one bucket per window (a selector polynomial's
+    coefficients are all equal): exercises the chunked combine levels (k_combine_level)."""
+    nbits = 16
+    path = f"/tmp/kgs_test_gpu_p{nbits}.ptau"
+    ctx = K.Context(0)
+    if not os.path.exists(path):
+        ctx.write_synthetic_ptau(path, nbits, common.tau())
+    ctx.load_ptau(path, nbits)
+    srs = P.SRS(path, common.tau())
+    rnd = random.Random(99)
+    a, b = rnd.randrange(R), rnd.randrange(R)
+    n = 1 << nbits
+    cases = {
+        "all-equal": [a] * n,
+        "minus-1/n (selector pattern)": [(-pow(n, -1, R)) % R] * n,
+        "two-valued": [a if i % 3 else b for i in range(n)],
+        "mostly-zero": [a if i % 1000 == 0 else 0 for i in range(n)],
+        "equal-then-random": [a] * (n // 2) + [rnd.randrange(R) for _ in range(n // 2)],
+        "all-equal-odd-length": [b] * (n - 3),
+    }
+    for name, v in cases.items():
+        assert ctx.msm(common.mont_bytes(v)) == bn.g1_to_lem(srs.msm(v)), name
+    ctx.close()
+
+
 @pytest.mark.parametrize("kind", [0, 1])
 @pytest.mark.parametrize("sel", [False, True])
 @pytest.mark.parametrize("nbits", [1, 4, 11, 13])
