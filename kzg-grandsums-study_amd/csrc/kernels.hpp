@@ -37,6 +37,7 @@ struct MsmWork {
   uint32_t *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *sorted = nullptr;
   uint32_t *bstart = nullptr, *segpart = nullptr, *buckets = nullptr, *part = nullptr;
   uint32_t* segowner = nullptr;  // bucket of each segment's first run
+  uint32_t* locnt = nullptr;     // lo pass: 256 partitions x 256 lo x 16 chunks counts / bases
 };
 
 // ntt.hip

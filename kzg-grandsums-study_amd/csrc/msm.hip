@@ -242,36 +242,81 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
   }
 }
 
-// one workgroup per partition p: counting sort by lo (tiles of SL_TILE through LDS), bucket
-// offsets for keys (p << lob) + lo
+// Pass 2: every partition p is cut into SL_G chunks; (1) per-chunk LDS histograms of lo, (2) one
+// workgroup per partition scans them into per-(lo, chunk) global bases and writes the bucket
+// offsets, (3) every chunk counting-sorts its entries tile by tile through LDS and writes runs.
+// Chunks keep a skewed partition (all points in one bucket: a selector polynomial's equal
+// coefficients) spread over SL_G workgroups instead of one.
 constexpr int SL_THREADS = 1024;
 constexpr int SL_TILE = 4096;
-__global__ void __launch_bounds__(SL_THREADS) k_sort_lo(uint32_t* __restrict__ sorted, uint32_t* __restrict__ offsets,
-                                                         const uint32_t* __restrict__ tval,
-                                                         const uint8_t* __restrict__ tlo,
-                                                         const uint32_t* __restrict__ hi_off, int lob, int NH,
-                                                         uint32_t B) {
-  __shared__ uint32_t cnt[256], cur[256], tcnt[256], toff[256];
+constexpr int SL_G = 16;
+
+__device__ __forceinline__ void chunk_range(uint32_t s0, uint32_t s1, int g, uint32_t& c0, uint32_t& c1) {
+  const uint32_t csz = (s1 - s0 + SL_G - 1) / SL_G;
+  c0 = s0 + g * csz < s1 ? s0 + g * csz : s1;
+  c1 = c0 + csz < s1 ? c0 + csz : s1;
+}
+
+// grid (SL_G, NH): locnt[(p * nb + lo) * SL_G + g] = #entries of chunk g of partition p with this lo
+__global__ void __launch_bounds__(SL_THREADS) k_lo_count(uint32_t* __restrict__ locnt, const uint8_t* __restrict__ tlo,
+                                                         const uint32_t* __restrict__ hi_off, int lob) {
+  __shared__ uint32_t cnt[256];
+  const int g = blockIdx.x, p = blockIdx.y;
+  const int nb = 1 << lob;
+  uint32_t c0, c1;
+  chunk_range(hi_off[p], hi_off[p + 1], g, c0, c1);
+  if ((int)threadIdx.x < nb) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t e = c0 + threadIdx.x; e < c1; e += SL_THREADS) atomicAdd(&cnt[tlo[e]], 1u);
+  __syncthreads();
+  if ((int)threadIdx.x < nb) locnt[((uint64_t)p * nb + threadIdx.x) * SL_G + g] = cnt[threadIdx.x];
+}
+
+// grid NH, 256 threads: bases (in place over locnt) and the bucket offsets of keys (p << lob) + lo + 1
+__global__ void __launch_bounds__(256) k_lo_scan(uint32_t* __restrict__ locnt, uint32_t* __restrict__ offsets,
+                                                 const uint32_t* __restrict__ hi_off, int lob) {
+  __shared__ uint32_t tot[256], pre[256];
+  const int p = blockIdx.x;
+  const int nb = 1 << lob;
+  const uint32_t lo = threadIdx.x;
+  uint32_t* row = locnt + ((uint64_t)p * nb + lo) * SL_G;
+  uint32_t run = 0;
+  if ((int)lo < nb)
+    for (int g = 0; g < SL_G; g++) {
+      const uint32_t v = row[g];
+      row[g] = run;
+      run += v;
+    }
+  tot[lo] = (int)lo < nb ? run : 0;
+  __syncthreads();
+  if (threadIdx.x < 64) wave_excl_scan256(tot, pre, nb);
+  __syncthreads();
+  if ((int)lo < nb) {
+    const uint32_t base = hi_off[p] + pre[lo];
+    offsets[((uint32_t)p << lob) + lo + 1] = base;
+    for (int g = 0; g < SL_G; g++) row[g] += base;
+  }
+}
+
+// grid (SL_G, NH): chunk g of partition p, tiles of SL_TILE through LDS, run-wise stores
+__global__ void __launch_bounds__(SL_THREADS) k_lo_scatter(uint32_t* __restrict__ sorted,
+                                                           const uint32_t* __restrict__ locnt,
+                                                           const uint32_t* __restrict__ tval,
+                                                           const uint8_t* __restrict__ tlo,
+                                                           const uint32_t* __restrict__ hi_off, int lob) {
+  __shared__ uint32_t cur[256], tcnt[256], toff[256];
   __shared__ uint32_t sv[SL_TILE];
   __shared__ uint8_t sl[SL_TILE];
-  const int p = blockIdx.x;
+  const int g = blockIdx.x, p = blockIdx.y;
   const uint32_t tid = threadIdx.x;
-  const int nb = 1 << lob;  // keys (p << lob) + 1 .. ((p + 1) << lob)
-  const uint32_t s0 = hi_off[p], s1 = hi_off[p + 1];
-  if ((int)tid < nb) cnt[tid] = 0;
+  const int nb = 1 << lob;
+  uint32_t c0, c1;
+  chunk_range(hi_off[p], hi_off[p + 1], g, c0, c1);
+  if (c0 >= c1) return;  // uniform per block
+  if ((int)tid < nb) cur[tid] = locnt[((uint64_t)p * nb + tid) * SL_G + g];
   __syncthreads();
-  for (uint32_t e = s0 + tid; e < s1; e += SL_THREADS) atomicAdd(&cnt[tlo[e]], 1u);
-  __syncthreads();
-  if (tid < 64) {
-    wave_excl_scan256(cnt, cur, nb);
-    for (int b = tid; b < nb; b += 64) {
-      cur[b] += s0;
-      offsets[((uint32_t)p << lob) + b + 1] = cur[b];
-    }
-  }
-  __syncthreads();
-  for (uint32_t t0 = s0; t0 < s1; t0 += SL_TILE) {
-    const uint32_t tn = s1 - t0 < (uint32_t)SL_TILE ? s1 - t0 : (uint32_t)SL_TILE;
+  for (uint32_t t0 = c0; t0 < c1; t0 += SL_TILE) {
+    const uint32_t tn = c1 - t0 < (uint32_t)SL_TILE ? c1 - t0 : (uint32_t)SL_TILE;
     if ((int)tid < nb) tcnt[tid] = 0;
     __syncthreads();
     uint32_t v[SL_TILE / SL_THREADS], r[SL_TILE / SL_THREADS];
@@ -514,8 +559,10 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
     default:
       return;  // choose_c keeps 7 <= c <= 17
   }
-  hipLaunchKernelGGL(k_sort_lo, dim3(NH), dim3(SL_THREADS), 0, st, w.sorted, w.offsets, (const uint32_t*)w.digit,
-                     w.lo, hi_off, lob, NH, B);
+  hipLaunchKernelGGL(k_lo_count, dim3(SL_G, NH), dim3(SL_THREADS), 0, st, w.locnt, w.lo, hi_off, lob);
+  hipLaunchKernelGGL(k_lo_scan, dim3(NH), dim3(256), 0, st, w.locnt, w.offsets, hi_off, lob);
+  hipLaunchKernelGGL(k_lo_scatter, dim3(SL_G, NH), dim3(SL_THREADS), 0, st, w.sorted, w.locnt,
+                     (const uint32_t*)w.digit, w.lo, hi_off, lob);
   if (ev) hipEventRecord(ev[1], st);
   const uint64_t E = N * (uint64_t)W;  // upper bound of nonzero entries
   uint64_t L = E >> 18;

@@ -272,6 +272,7 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
   c.mw.bstart = c.buf("msm_bstart", 128 * (size_t)(B + 2));
   c.mw.segpart = c.buf("msm_segpart", 128 * nseg);
   c.mw.segowner = c.buf("msm_segowner", 4 * nseg);
+  c.mw.locnt = c.buf("msm_locnt", 4 * 256 * 256 * 16);
   c.mw.buckets = c.buf("msm_buckets", 128 * (size_t)(B + 2));
   const uint32_t chunks = (B / 2 + 255) / 256 > 0 ? (B / 2 + 255) / 256 : 1;
   c.mw.part = c.buf("msm_part", 128 * (size_t)cc * chunks);
