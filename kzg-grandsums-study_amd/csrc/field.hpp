@@ -141,7 +141,8 @@ struct Fe {
         : "v"(x0), "v"(y0), "v"(x1), "v"(y1));
 #endif
   }
-  __device__ __forceinline__ friend Fe operator*(const Fe& A, const Fe& B) {
+  // product in [0, 2p) for inputs in [0, 2p) (p < 2^254, so 4p < R = 2^256)
+  __device__ __forceinline__ static Fe mul_nored(const Fe& A, const Fe& B) {
     const uint32_t* a = A.v;
     const uint32_t* b = B.v;
     uint32_t m[8];
@@ -167,10 +168,49 @@ struct Fe {
       t2 = 0;
     }
     r.v[7] = (uint32_t)acc;
-    return reduce_once(r);
+    return r;
   }
+  __device__ __forceinline__ friend Fe operator*(const Fe& A, const Fe& B) { return reduce_once(mul_nored(A, B)); }
 
   __device__ __forceinline__ Fe sqr() const { return (*this) * (*this); }
+
+  // ---- lazy reduction on [0, 2p): the bucket-accumulation chain keeps its point in this range
+  // (one conditional subtraction per product saved) and canonicalises once per emitted run
+  __device__ __forceinline__ static constexpr uint32_t p2(int i) {
+    return (P::p[i] << 1) | (i ? P::p[i - 1] >> 31 : 0u);
+  }
+  __device__ __forceinline__ static Fe add_lazy(const Fe& a, const Fe& b) {
+    Fe s, d;
+    uint32_t c = 0, borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);  // < 4p < 2^256
+#pragma unroll
+    for (int i = 0; i < 8; i++) d.v[i] = __builtin_subc(s.v[i], p2(i), borrow, &borrow);
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = borrow ? s.v[i] : d.v[i];
+    return s;
+  }
+  __device__ __forceinline__ static Fe sub_lazy(const Fe& a, const Fe& b) {
+    Fe d, e;
+    uint32_t borrow = 0, c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) d.v[i] = __builtin_subc(a.v[i], b.v[i], borrow, &borrow);
+#pragma unroll
+    for (int i = 0; i < 8; i++) e.v[i] = __builtin_addc(d.v[i], p2(i), c, &c);
+#pragma unroll
+    for (int i = 0; i < 8; i++) d.v[i] = borrow ? e.v[i] : d.v[i];
+    return d;
+  }
+  __device__ __forceinline__ bool is_zero_lazy() const {  // == 0 mod p for a value in [0, 2p)
+    uint32_t z = 0, q = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      z |= v[i];
+      q |= v[i] ^ P::p[i];
+    }
+    return z == 0 || q == 0;
+  }
+  __device__ __forceinline__ Fe canon() const { return reduce_once(*this); }
 
   __device__ __forceinline__ Fe to_mont() const {
     Fe r2;
@@ -322,6 +362,33 @@ struct g1_xyzz {
     X = nX;
     ZZ = ZZ * PP;
     ZZZ = ZZZ * PPP;
+  }
+
+  // madd-2008-s with the accumulator kept lazily reduced (coordinates in [0, 2q)); the affine
+  // input is canonical. Same special cases as add_aff. Call canon() before storing.
+  __device__ __forceinline__ void add_aff_lazy(const g1_aff& a) {
+    if (a.is_inf()) return;
+    if (is_inf()) { *this = from_aff(a); return; }
+    fq U2 = fq::mul_nored(a.x, ZZ);
+    fq S2 = fq::mul_nored(a.y, ZZZ);
+    fq P = fq::sub_lazy(U2, X);
+    fq R = fq::sub_lazy(S2, Y);
+    if (P.is_zero_lazy()) {
+      if (R.is_zero_lazy()) { *this = dbl_aff(a); return; }
+      *this = inf();
+      return;
+    }
+    fq PP = fq::mul_nored(P, P);
+    fq PPP = fq::mul_nored(P, PP);
+    fq Qv = fq::mul_nored(X, PP);
+    fq nX = fq::sub_lazy(fq::sub_lazy(fq::mul_nored(R, R), PPP), fq::add_lazy(Qv, Qv));
+    Y = fq::sub_lazy(fq::mul_nored(R, fq::sub_lazy(Qv, nX)), fq::mul_nored(Y, PPP));
+    X = nX;
+    ZZ = fq::mul_nored(ZZ, PP);
+    ZZZ = fq::mul_nored(ZZZ, PPP);
+  }
+  __device__ __forceinline__ void canon() {
+    X = X.canon(); Y = Y.canon(); ZZ = ZZ.canon(); ZZZ = ZZZ.canon();
   }
 
   // add-2008-s: this += other

@@ -392,6 +392,7 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
   g1_xyzz acc = g1_xyzz::inf();
   for (uint64_t e = start; e < end; e++) {
     if (e >= bend) {
+      acc.canon();
       emit_run(bstart, segpart, b, rs, offsets, s, acc);
       do { b++; bend = offsets[b + 1]; } while (e >= bend);
       rs = e;
@@ -400,8 +401,13 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
     uint32_t v = sorted[e];
     g1_aff p = g1_aff::load(table + 16 * (uint64_t)(v & 0x7fffffffu));
     if (v & 0x80000000u) p.y = p.y.neg();
+#ifdef KGS_NO_LAZY
     acc.add_aff(p);
+#else
+    acc.add_aff_lazy(p);
+#endif
   }
+  acc.canon();
   emit_run(bstart, segpart, b, rs, offsets, s, acc);
 }
 
