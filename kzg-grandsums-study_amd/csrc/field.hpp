@@ -141,6 +141,21 @@ struct Fe {
         : "v"(x0), "v"(y0), "v"(x1), "v"(y1));
 #endif
   }
+  // first mac(s) of a column: the carry word is WRITTEN (0 + 0 + carry), saving its zeroing move
+  __device__ __forceinline__ static void mac_init(uint64_t& acc, uint32_t& t2, uint32_t x, uint32_t y) {
+    uint64_t c;
+    asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_addc_co_u32 %1, %2, 0, 0, %2"
+        : "+v"(acc), "=v"(t2), "=&s"(c)
+        : "v"(x), "v"(y));
+  }
+  __device__ __forceinline__ static void mac2_init(uint64_t& acc, uint32_t& t2, uint32_t x0, uint32_t y0, uint32_t x1,
+                                                   uint32_t y1) {
+    uint64_t c0, c1;
+    asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n\tv_addc_co_u32 %1, %2, 0, 0, %2\n\t"
+        "v_mad_u64_u32 %0, %3, %6, %7, %0\n\tv_addc_co_u32 %1, %3, 0, %1, %3"
+        : "+v"(acc), "=&v"(t2), "=&s"(c0), "=&s"(c1)
+        : "v"(x0), "v"(y0), "v"(x1), "v"(y1));
+  }
   // product in [0, 2p) for inputs in [0, 2p) (p < 2^254, so 4p < R = 2^256)
   __device__ __forceinline__ static Fe mul_nored(const Fe& A, const Fe& B) {
     const uint32_t* a = A.v;
@@ -148,28 +163,33 @@ struct Fe {
     uint32_t m[8];
     Fe r;
     uint64_t acc = 0;
-    uint32_t t2 = 0;
+    uint32_t t2;  // carry word of the current column: written (not accumulated) by its first mac
 #pragma unroll
     for (int i = 0; i < 8; i++) {
+      if (i == 0) {
+        mac_init(acc, t2, a[0], b[0]);
+      } else {
+        mac2_init(acc, t2, a[0], b[i], m[0], P::p[i]);
 #pragma unroll
-      for (int j = 0; j < i; j++) mac2(acc, t2, a[j], b[i - j], m[j], P::p[i - j]);
-      mac(acc, t2, a[i], b[0]);
+        for (int j = 1; j < i; j++) mac2(acc, t2, a[j], b[i - j], m[j], P::p[i - j]);
+        mac(acc, t2, a[i], b[0]);
+      }
       m[i] = (uint32_t)acc * P::inv;
       mac(acc, t2, m[i], P::p[0]);
       acc = (acc >> 32) | ((uint64_t)t2 << 32);
-      t2 = 0;
     }
 #pragma unroll
     for (int i = 8; i < 15; i++) {
+      mac2_init(acc, t2, a[i - 7], b[7], m[i - 7], P::p[7]);
 #pragma unroll
-      for (int j = i - 7; j < 8; j++) mac2(acc, t2, a[j], b[i - j], m[j], P::p[i - j]);
+      for (int j = i - 6; j < 8; j++) mac2(acc, t2, a[j], b[i - j], m[j], P::p[i - j]);
       r.v[i - 8] = (uint32_t)acc;
       acc = (acc >> 32) | ((uint64_t)t2 << 32);
-      t2 = 0;
     }
     r.v[7] = (uint32_t)acc;
     return r;
   }
+
   __device__ __forceinline__ friend Fe operator*(const Fe& A, const Fe& B) { return reduce_once(mul_nored(A, B)); }
 
   __device__ __forceinline__ Fe sqr() const { return (*this) * (*this); }
