@@ -480,7 +480,10 @@ __global__ void __launch_bounds__(256) k_combine(uint32_t* __restrict__ buckets,
 // 1 at bit k of t), T_{c-1} = S_B. Block (chunk, k): every thread first adds BS_CHAIN buckets in
 // sequence (all lanes busy), then one LDS tree over the 256 thread sums (the active lanes stay
 // packed in the low waves, so the tree costs ~9 wave-adds instead of 6 per wave with shuffles).
-constexpr int BS_CHAIN = 8;
+#ifndef KGS_BS_CHAIN
+#define KGS_BS_CHAIN 8
+#endif
+constexpr int BS_CHAIN = KGS_BS_CHAIN;
 constexpr uint32_t BS_SPAN = 256 * BS_CHAIN;  // buckets per block
 
 __device__ __forceinline__ g1_xyzz block_tree_sum256(g1_xyzz v, uint32_t* lds) {
