@@ -84,6 +84,20 @@ def max_over_ranks(t):
     return float(te.item())
 
 
+def shared_ptau(ctx, nbits, dist):
+    """Synthetic ptau of power `nbits`, written once per node by the product's GPU writer (rank 0
+    writes to a temporary name and renames atomically; the other ranks wait at a barrier)."""
+    path = f"/tmp/kgs_bench_p{nbits}.ptau"
+    t0 = time.time()
+    if int(os.environ.get("LOCAL_RANK", "0")) == 0 and not os.path.exists(path):
+        tmp = f"{path}.{os.getpid()}.tmp"
+        ctx.write_synthetic_ptau(tmp, nbits, bench_tau())
+        os.replace(tmp, path)
+    if dist:
+        dist.barrier()
+    return path, time.time() - t0
+
+
 def selected_vector_leg(K, torch, dist, rank, world, local, args):
     """BASELINE configs[4] / SURVEY C5: selected-vector grand-sum, k = 4, n = 2^22 (selF = ones but
     the last, selT = ones but the first, T = rot(F)); same inputs on every rank. N > 1: MSMs
@@ -91,10 +105,8 @@ def selected_vector_leg(K, torch, dist, rank, world, local, args):
     nb, k = args.sv_nbits, 4
     n = 1 << nb
     ctx = K.Context(local)
-    ptau = f"/tmp/kgs_bench_p{nb}_r{rank}.ptau"
     t0 = time.time()
-    if not os.path.exists(ptau):
-        ctx.write_synthetic_ptau(ptau, nb, bench_tau())
+    ptau, _ = shared_ptau(ctx, nb, dist)
     ctx.load_ptau(ptau, nb)
     setup_s = time.time() - t0
     keep, d_f, d_t = [], [], []
@@ -176,11 +188,7 @@ def main():
     nbits = args.nbits
     n = 1 << nbits
     kind = K.GRANDSUM if args.kind == "grandsum" else K.GRANDPRODUCT
-    ptau = f"/tmp/kgs_bench_p{nbits}_r{rank}.ptau"
-    t_srs = time.time()
-    if not os.path.exists(ptau):
-        ctx.write_synthetic_ptau(ptau, nbits, bench_tau())
-    t_gen = time.time() - t_srs
+    ptau, t_gen = shared_ptau(ctx, nbits, dist)
     t0 = time.time()
     ctx.load_ptau(ptau, nbits)
     for c in extra:
@@ -245,7 +253,7 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
 
     # ---------------- extra configs (BASELINE.json configs[2] and [4]), outside the timed region
-    extra = {}
+    extra_cfg = {}
     if args.extra_legs:
         # C3: grand-product at the same n, same contexts / inputs (replicas per GPU)
         gp_steps = 4 * len(ctxs)
@@ -259,7 +267,7 @@ def main():
         steps(gp_steps)
         torch.cuda.synchronize()
         el = max_over_ranks(time.perf_counter() - t1)
-        extra["grandproduct_vs_grandsum" if kind_main == K.GRANDSUM else "grandsum_vs_grandproduct"] = {
+        extra_cfg["grandproduct_vs_grandsum" if kind_main == K.GRANDSUM else "grandsum_vs_grandproduct"] = {
             "workload": f"{'grandproduct' if kind == K.GRANDPRODUCT else 'grandsum'} prover, n=2^{nbits}, k={args.npols}, no selectors",
             "proofs_per_s": round(gp_steps * world / el, 4), "proofs": gp_steps * world}
         kind = kind_main
@@ -267,7 +275,7 @@ def main():
         for c in ctxs[1:]:
             c.close()
         ctxs[1:] = []
-        extra["selected_vector"] = selected_vector_leg(K, torch, dist, rank, world, local, args)
+        extra_cfg["selected_vector"] = selected_vector_leg(K, torch, dist, rank, world, local, args)
 
     if rank != 0:
         if dist:
@@ -361,7 +369,7 @@ def main():
         "msm": msm,
         "roofline": roofline,
         "hbm_view": hbm_view,
-        "extra_configs": extra,
+        "extra_configs": extra_cfg,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out))
