@@ -229,8 +229,14 @@ def main():
         for x in th:
             x.join()
 
+    # throughput contexts: one MSM lane each (the in-flight proofs keep the GPU busy); the
+    # single-proof latency below uses context 0 with two lanes (kgs_ctx_set_msm_lanes)
+    for c in ctxs:
+        c.set_msm_lanes(1 if len(ctxs) > 1 else 2)
     steps(max(args.warmup, len(ctxs)))
-    # single-stream latency (one proof at a time on one context), outside the timed region
+    # single-proof latency (one proof at a time on one context), outside the timed region
+    ctx.set_msm_lanes(2)
+    run(0, 1)
     t_lat = []
     for _ in range(3):
         t1 = time.perf_counter()
@@ -238,6 +244,7 @@ def main():
         t_lat.append(time.perf_counter() - t1)
     latency_ms = 1000.0 * min(t_lat)
     rounds = ctx.last_timing()
+    ctx.set_msm_lanes(1 if len(ctxs) > 1 else 2)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()

@@ -67,6 +67,13 @@ int kgs_shard_range(uint64_t n, int rank, int world, uint64_t* lo, uint64_t* hi)
  * X,Y,ZZ,ZZZ LE Montgomery Fq, ZZ == 0 is infinity): sum_k 2^k sum_r T_k^(r) -> affine LEM */
 int kgs_msm_combine(const uint8_t* T_all, int nparts, int c, uint8_t out_lem[64]);
 
+/* MSM lanes per context (default 2): with 2, the independent commitments of one prover round
+ * (round 1's F_i / T_i, round 5's W_xi / W_xiw) alternate between two HIP streams with separate
+ * work buffers, so one MSM's latency-bound tail overlaps the other's bucket accumulation
+ * (single-proof latency -3 %, selected-vector 2^22 k=4 -7 %). Use 1 when several contexts already
+ * keep the GPU busy with independent proofs (throughput). */
+int kgs_ctx_set_msm_lanes(kgs_ctx_t* ctx, int lanes);
+
 /* Load a .ptau file (binfileutils layout, sections 1-3) and make the first 2^(nbits_max+1) G1
  * points device-resident, together with the MSM window tables and the NTT tables for domains
  * up to 2^nbits_max (nbits_max < 0: the file's power). Replaces readBinFile + readPTauHeader +

@@ -81,6 +81,7 @@ def lib():
         L.kgs_verify_ptau.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_u8p,
                                       c_u8p]
         L.kgs_ctx_set_shard.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.kgs_ctx_set_msm_lanes.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.kgs_shard_range.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_uint64)]
         L.kgs_msm_combine.argtypes = [c_u8p, ctypes.c_int, ctypes.c_int, c_u8p]
@@ -208,6 +209,10 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+    def set_msm_lanes(self, lanes):
+        """1 or 2 HIP streams for the independent MSMs of a prover round (kgs_ctx_set_msm_lanes)."""
+        _check(lib().kgs_ctx_set_msm_lanes(self._h, lanes))
 
     def set_shard(self, rank, world, allgather=None):
         """MSM point-range sharding (kgs_ctx_set_shard): `allgather(bytes) -> world * bytes`

@@ -87,6 +87,13 @@ struct kgs_ctx {
   int nbits_max = -1;
   MsmTables tb;
   MsmWork mw;
+  // second MSM lane: independent commitments of one round (R1's F_i/T_i, R5's two W) alternate
+  // between st and st2 (own work buffers), so one MSM's latency-bound tail overlaps the other's
+  // bucket accumulation
+  hipStream_t st2 = nullptr;
+  hipEvent_t ev_fork = nullptr;
+  MsmWork mw2;
+  int msm_lanes = 2;  // kgs_ctx_set_msm_lanes
   uint64_t msm_nseg_max = 0;
   // domain tables (M = 2^logM)
   int logM = -1;
@@ -103,6 +110,9 @@ struct kgs_ctx {
     if (st) hipStreamSynchronize(st);
     for (auto& kv : pool) hipFree(kv.second.p);
     if (h_pin) hipHostFree(h_pin);
+    if (st2) hipStreamSynchronize(st2);
+    if (ev_fork) hipEventDestroy(ev_fork);
+    if (st2) hipStreamDestroy(st2);
     if (st) hipStreamDestroy(st);
   }
 
@@ -147,7 +157,10 @@ struct kgs_ctx {
     HC(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
     return d;
   }
-  void sync() { HC(hipStreamSynchronize(st)); }
+  void sync() {
+    HC(hipStreamSynchronize(st));
+    if (st2) HC(hipStreamSynchronize(st2));
+  }
   void reset_staging() {
     sync();
     h_pin_off = 0;
@@ -262,20 +275,24 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
   uint64_t nseg = (1ull << 18) + (1ull << 16) + 2;
   if (E / 64 + 2 > nseg) nseg = E / 64 + 2;
   c.msm_nseg_max = nseg;
-  c.mw.digit = (int32_t*)c.buf("msm_digit", E * 4);
-  c.mw.sorted = c.buf("msm_sorted", E * 4);
-  c.mw.lo = (uint8_t*)c.buf("msm_lo", E);
-  c.mw.blockhist = c.buf("msm_blockhist", 4 * 264 * ((npts + 255) / 256 + 1));
-  c.mw.counts = c.buf("msm_counts", 4 * (B + 300));
-  c.mw.offsets = c.buf("msm_offsets", 4 * (B + 4));
-  c.mw.cursor = c.buf("msm_cursor", 4 * (B + 600));
-  c.mw.bstart = c.buf("msm_bstart", 128 * (size_t)(B + 2));
-  c.mw.segpart = c.buf("msm_segpart", 128 * nseg);
-  c.mw.segowner = c.buf("msm_segowner", 4 * nseg);
-  c.mw.locnt = c.buf("msm_locnt", 4 * 256 * 256 * 16);
-  c.mw.buckets = c.buf("msm_buckets", 128 * (size_t)(B + 2));
-  const uint32_t chunks = (B / 2 + 255) / 256 > 0 ? (B / 2 + 255) / 256 : 1;
-  c.mw.part = c.buf("msm_part", 128 * (size_t)cc * chunks);
+  for (int lane = 0; lane < 2; lane++) {
+    MsmWork& w = lane ? c.mw2 : c.mw;
+    const std::string sfx = lane ? "_2" : "";
+    w.digit = (int32_t*)c.buf("msm_digit" + sfx, E * 4);
+    w.sorted = c.buf("msm_sorted" + sfx, E * 4);
+    w.lo = (uint8_t*)c.buf("msm_lo" + sfx, E);
+    w.blockhist = c.buf("msm_blockhist" + sfx, 4 * 264 * ((npts + 255) / 256 + 1));
+    w.counts = c.buf("msm_counts" + sfx, 4 * (B + 300));
+    w.offsets = c.buf("msm_offsets" + sfx, 4 * (B + 4));
+    w.cursor = c.buf("msm_cursor" + sfx, 4 * (B + 600));
+    w.bstart = c.buf("msm_bstart" + sfx, 128 * (size_t)(B + 2));
+    w.segpart = c.buf("msm_segpart" + sfx, 128 * nseg);
+    w.segowner = c.buf("msm_segowner" + sfx, 4 * nseg);
+    w.locnt = c.buf("msm_locnt" + sfx, 4 * 256 * 256 * 16);
+    w.buckets = c.buf("msm_buckets" + sfx, 128 * (size_t)(B + 2));
+    const uint32_t chunks = (B / 2 + 255) / 256 > 0 ? (B / 2 + 255) / 256 : 1;
+    w.part = c.buf("msm_part" + sfx, 128 * (size_t)cc * chunks);
+  }
   c.srs_power = power;
   c.nbits_max = nbits_max;
   ensure_domain(c, nbits_max + 1);
@@ -297,7 +314,13 @@ void shard_range(uint64_t n, int rank, int world, uint64_t& lo, uint64_t& hi) {
   hi = (uint64_t)((unsigned __int128)n * (unsigned)(rank + 1) / (unsigned)world);
 }
 
-Commit commit_launch(kgs_ctx& c, const uint32_t* scalars, uint64_t N, int slot) {
+// the second MSM lane starts after everything issued so far on the main stream (the round's inputs)
+void fork_lanes(kgs_ctx& c) {
+  HC(hipEventRecord(c.ev_fork, c.st));
+  HC(hipStreamWaitEvent(c.st2, c.ev_fork, 0));
+}
+
+Commit commit_launch(kgs_ctx& c, const uint32_t* scalars, uint64_t N, int slot, int lane = 0) {
   Commit cm;
   cm.N = N;
   const int cc = c.tb.c;
@@ -313,9 +336,11 @@ Commit commit_launch(kgs_ctx& c, const uint32_t* scalars, uint64_t N, int slot) 
   }
   MsmTables tb = c.tb;
   tb.table += (size_t)16 * lo;  // same window stride (npts), points [lo, hi)
-  msm_run(c.st, tb, c.mw, scalars + (size_t)8 * lo, hi - lo, dT);
+  if (c.msm_lanes < 2) lane = 0;
+  hipStream_t st = lane ? c.st2 : c.st;  // lane 1 was forked (fork_lanes) after the round's inputs
+  msm_run(st, tb, lane ? c.mw2 : c.mw, scalars + (size_t)8 * lo, hi - lo, dT);
   check_launch();
-  HC(hipMemcpyAsync(cm.h_T, dT, (size_t)cc * 128, hipMemcpyDeviceToHost, c.st));
+  HC(hipMemcpyAsync(cm.h_T, dT, (size_t)cc * 128, hipMemcpyDeviceToHost, st));
   return cm;
 }
 
@@ -484,13 +509,14 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   }
   std::vector<Commit> r1;
   int slot = 0;
+  fork_lanes(c);
   for (int i = 0; i < k; i++) {
-    r1.push_back(commit_launch(c, Fc[i], n, slot++));
-    r1.push_back(commit_launch(c, Tc[i], n, slot++));
+    r1.push_back(commit_launch(c, Fc[i], n, slot++, 0));
+    r1.push_back(commit_launch(c, Tc[i], n, slot++, 1));
   }
   if (sel) {
-    r1.push_back(commit_launch(c, sFc, n, slot++));
-    r1.push_back(commit_launch(c, sTc, n, slot++));
+    r1.push_back(commit_launch(c, sFc, n, slot++, 0));
+    r1.push_back(commit_launch(c, sTc, n, slot++, 1));
   }
   c.sync();
   const int ncom = 2 * k + (sel ? 2 : 0) + 4;
@@ -730,8 +756,9 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   launch_divide(c.st, Wxw, flags + 3, P2, n, xpowers(c, xiw), c.buf("div_part2", 32 * (ntiles + 1)),
                 c.buf("div_carry2", 32 * (ntiles + 1)));
   check_launch();
-  Commit cW1 = commit_launch(c, Wx, L - 1, slot++);
-  Commit cW2 = commit_launch(c, Wxw, n - 1, slot++);
+  fork_lanes(c);
+  Commit cW1 = commit_launch(c, Wx, L - 1, slot++, 0);
+  Commit cW2 = commit_launch(c, Wxw, n - 1, slot++, 1);
   HC(hipMemcpyAsync(h_flags, flags, 64, hipMemcpyDeviceToHost, c.st));
   c.sync();
   if (h_flags[2] || h_flags[3]) throw KgsError(KGS_E_DOES_NOT_DIVIDE, "Polynomial does not divide");
@@ -843,6 +870,8 @@ int kgs_ctx_create(int device, kgs_ctx_t** out) {
     auto* c = new kgs_ctx();
     c->device = device;
     HC(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    HC(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
+    HC(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     c->d_scal = c->buf("scalars", kgs_ctx::SCAL_BYTES);
     c->ensure_pin(8 << 20);
     *out = c;
@@ -1124,6 +1153,13 @@ int kgs_ctx_set_shard(kgs_ctx_t* ctx, int rank, int world, kgs_allgather_fn fn, 
   ctx->shard_world = world;
   ctx->shard_fn = world > 1 ? fn : nullptr;
   ctx->shard_user = world > 1 ? user : nullptr;
+  API_END
+}
+
+int kgs_ctx_set_msm_lanes(kgs_ctx_t* ctx, int lanes) {
+  API_BEGIN
+  if (!ctx || lanes < 1 || lanes > 2) throw KgsError(KGS_E_ARG, "msm lanes must be 1 or 2");
+  ctx->msm_lanes = lanes;
   API_END
 }
 
