@@ -17,9 +17,15 @@ N > 1 GPUs (torchrun, one process per GPU): every rank proves its own independen
 (replicas, "weak" scaling); value = proofs of all ranks / max-over-ranks time.
 
 Extra fields in the JSON line:
-  msm       : live HIP-event timing of the MSM phases at N = n points (points/s, G1 adds/s)
+  proof_verified : one proof of the timed workload checked with the native verifier (pairing)
+  latency_ms_single_proof / round_ms_single_proof : one proof at a time on one context (2 MSM lanes)
+  msm       : live HIP-event timing of the MSM phases at N = n (points/s, G1 adds/s)
   roofline  : the dominant kernel (MSM bucket accumulation, k_accumulate) against the INT-VALU
-              Montgomery-product roof; traffic from profiles/ PMC summary
+              Montgomery-product roof; traffic = PMC FETCH+WRITE from profiles/
+  hbm_view  : proof-level bytes (SURVEY.md §8d's count over the reference op list) per second vs 8 TB/s
+  extra_configs : BASELINE.json configs[2] (grand-product at n), configs[3] (grand-sum n = 2^24) and
+              configs[4] (selected-vector k = 4, n = 2^22) — single GPU at N = 1, every MSM
+              point-range sharded over all ranks at N > 1 (strong scaling); each checks a proof
   cpu_baseline : the CPU port of the reference op list (oracle/c, OpenMP) on the same workload
 """
 import argparse
@@ -98,11 +104,11 @@ def shared_ptau(ctx, nbits, dist):
     return path, time.time() - t0
 
 
-def selected_vector_leg(K, torch, dist, rank, world, local, args):
-    """BASELINE configs[4] / SURVEY C5: selected-vector grand-sum, k = 4, n = 2^22 (selF = ones but
-    the last, selT = ones but the first, T = rot(F)); same inputs on every rank. N > 1: MSMs
-    point-range sharded over all ranks (kgs_ctx_set_shard over torch.distributed = RCCL)."""
-    nb, k = args.sv_nbits, 4
+def large_leg(K, torch, dist, rank, world, local, nb, k, selected, proofs, label):
+    """One large configuration (BASELINE configs[3] / [4]: SURVEY C4 / C5), same inputs on every
+    rank: N = 1 on one GPU; N > 1 with every MSM point-range sharded over all ranks
+    (kgs_ctx_set_shard over torch.distributed = RCCL). The last proof is checked with the native
+    verifier (kgs_verify_ptau: transcript replay + pairing)."""
     n = 1 << nb
     ctx = K.Context(local)
     t0 = time.time()
@@ -117,28 +123,36 @@ def selected_vector_leg(K, torch, dist, rank, world, local, args):
         keep += [tf, tt]
         d_f.append(tf.data_ptr())
         d_t.append(tt.data_ptr())
-    one = np.frombuffer(K.FR_ONE_MONT, dtype=np.uint8)
-    sf = np.tile(one, n)
-    st = sf.copy()
-    sf[32 * (n - 1):] = 0
-    st[:32] = 0
-    tsf = torch.from_numpy(sf).to(f"cuda:{local}")
-    tst = torch.from_numpy(st).to(f"cuda:{local}")
+        del f, t
+    sfp = stp = None
+    if selected:  # selF = ones but the last, selT = ones but the first
+        one = np.frombuffer(K.FR_ONE_MONT, dtype=np.uint8)
+        sf = np.tile(one, n)
+        st = sf.copy()
+        sf[32 * (n - 1):] = 0
+        st[:32] = 0
+        tsf = torch.from_numpy(sf).to(f"cuda:{local}")
+        tst = torch.from_numpy(st).to(f"cuda:{local}")
+        keep += [tsf, tst]
+        sfp, stp = tsf.data_ptr(), tst.data_ptr()
+        del sf, st
     if world > 1:
         ctx.set_shard(rank, world, K.torch_allgather(device=None if BACKEND == "gloo" else f"cuda:{local}"))
-    ctx.prove_device(K.GRANDSUM, nb, d_f, d_t, tsf.data_ptr(), tst.data_ptr())  # warm-up
+    ctx.prove_device(K.GRANDSUM, nb, d_f, d_t, sfp, stp)  # warm-up
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    for _ in range(args.sv_proofs):
-        coms = ctx.prove_device(K.GRANDSUM, nb, d_f, d_t, tsf.data_ptr(), tst.data_ptr())[0]
+    for _ in range(proofs):
+        coms, evs = ctx.prove_device(K.GRANDSUM, nb, d_f, d_t, sfp, stp)
     torch.cuda.synchronize()
     el = max_over_ranks(time.perf_counter() - t1)
-    out = {"workload": f"selected-vector grand-sum, n=2^{nb}, k={k}, selectors", "n_gpus": world,
+    cn, en = K.proof_names(K.GRANDSUM, k, selected)
+    verified = K.grandsum_verifier(ptau, {"commitments": dict(zip(cn, coms)), "evaluations": dict(zip(en, evs))}, nb)
+    out = {"workload": label, "n_gpus": world,
            "mode": "msm point-range sharded (strong scaling)" if world > 1 else "single GPU",
-           "proofs": args.sv_proofs, "ms_per_proof": round(1000.0 * el / args.sv_proofs, 3),
-           "proofs_per_s": round(args.sv_proofs / el, 4), "srs_setup_s": round(setup_s, 2)}
+           "proofs": proofs, "ms_per_proof": round(1000.0 * el / proofs, 3),
+           "proofs_per_s": round(proofs / el, 4), "srs_setup_s": round(setup_s, 2), "proof_verified": verified}
     if dist:
         h = torch.tensor(list(K.keccak256(b"".join(coms))[:8]), dtype=torch.int64, device=coll_device())
         hs = [torch.empty_like(h) for _ in range(world)]
@@ -146,6 +160,8 @@ def selected_vector_leg(K, torch, dist, rank, world, local, args):
         out["ranks_agree"] = all(bool(torch.equal(hs[0], x)) for x in hs)
     ctx.set_shard(0, 1)
     ctx.close()
+    del keep
+    torch.cuda.empty_cache()
     return out
 
 
@@ -161,8 +177,11 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--msm-reps", type=int, default=5)
     ap.add_argument("--no-extra-legs", dest="extra_legs", action="store_false",
-                    help="skip the grand-product (configs[2]) and selected-vector 2^22 (configs[4]) legs")
+                    help="skip the grand-product (configs[2]), grand-sum 2^24 (configs[3]) and selected-vector "
+                         "2^22 (configs[4]) legs")
     ap.add_argument("--sv-nbits", type=int, default=22)
+    ap.add_argument("--c4-nbits", type=int, default=24, help="configs[3] leg (0 = skip)")
+    ap.add_argument("--c4-proofs", type=int, default=3)
     ap.add_argument("--sv-proofs", type=int, default=3,
                     help="proofs timed in the selected-vector leg (N > 1: MSMs sharded over all ranks)")
     ap.add_argument("--inflight", type=int, default=4,
@@ -244,6 +263,12 @@ def main():
         t_lat.append(time.perf_counter() - t1)
     latency_ms = 1000.0 * min(t_lat)
     rounds = ctx.last_timing()
+    # the proofs the bench times are real: check one with the native verifier (pairing)
+    d_f0, d_t0 = bufs[0]
+    coms0, evs0 = ctx.prove_device(kind, nbits, d_f0, d_t0)
+    cn0, en0 = K.proof_names(kind, args.npols, False)
+    vf = K.grandsum_verifier if kind == K.GRANDSUM else K.grandproduct_verifier
+    proof_verified = vf(ptau, {"commitments": dict(zip(cn0, coms0)), "evaluations": dict(zip(en0, evs0))}, nbits)
     ctx.set_msm_lanes(1 if len(ctxs) > 1 else 2)
     if dist:
         dist.barrier()
@@ -282,7 +307,11 @@ def main():
         for c in ctxs[1:]:
             c.close()
         ctxs[1:] = []
-        extra_cfg["selected_vector"] = selected_vector_leg(K, torch, dist, rank, world, local, args)
+        extra_cfg["selected_vector"] = large_leg(K, torch, dist, rank, world, local, args.sv_nbits, 4, True,
+                                                 args.sv_proofs, f"selected-vector grand-sum, n=2^{args.sv_nbits}, k=4, selectors")
+        if args.c4_nbits > 0:
+            extra_cfg["large_grandsum"] = large_leg(K, torch, dist, rank, world, local, args.c4_nbits, 1, False,
+                                                    args.c4_proofs, f"grand-sum, n=2^{args.c4_nbits}, k=1, no selectors")
 
     if rank != 0:
         if dist:
@@ -371,6 +400,7 @@ def main():
                    "nbits": nbits, "npols": args.npols, "selectors": False, "parallelism": f"replicas x{world}", "inflight_per_gpu": args.inflight,
                    "srs_power": power, "srs_points_resident": npts, "srs_gen_s": round(t_gen, 2),
                    "srs_load_s": round(t_load, 2)},
+        "proof_verified": proof_verified,
         "latency_ms_single_proof": round(latency_ms, 3),
         "round_ms_single_proof": [round(x, 3) for x in rounds],
         "msm": msm,
