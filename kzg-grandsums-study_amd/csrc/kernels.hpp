@@ -38,6 +38,8 @@ struct MsmWork {
   uint32_t *bstart = nullptr, *segpart = nullptr, *buckets = nullptr, *part = nullptr;
   uint32_t* segowner = nullptr;  // bucket of each segment's first run
   uint32_t* locnt = nullptr;     // lo pass: 256 partitions x 256 lo x 16 chunks counts / bases
+  uint32_t* chunklist = nullptr; // combine levels: 3 lists of chunk-start segments
+  uint32_t* chunkcnt = nullptr;  // their lengths
 };
 
 // ntt.hip

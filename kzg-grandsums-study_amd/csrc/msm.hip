@@ -358,6 +358,20 @@ __global__ void __launch_bounds__(SL_THREADS) k_lo_scatter(uint32_t* __restrict_
 }
 
 // ------------------------------------------------------------------ bucket accumulation
+constexpr uint32_t CB_T = 16;  // partials per thread per combine level
+constexpr int CB_LEVELS = 3;
+
+// Segment s (first run inside bucket [o0, o1)) starts a level chunk of `stride` partials x CB_T
+// when its bucket has more than CB_T partials and s is aligned: append it to that level's list.
+__device__ __forceinline__ void combine_enqueue(uint32_t* list, uint32_t* cnt, uint64_t s, uint64_t o0, uint64_t o1,
+                                                uint32_t L, uint64_t stride) {
+  if (s * L <= o0) return;  // the segment's first run starts its bucket (bstart), not a partial
+  const uint64_t s_lo = o0 / L + 1, s_hi = (o1 + L - 1) / L;
+  if (s_hi - s_lo <= CB_T) return;  // short list: summed directly by k_combine
+  if ((s - s_lo) % (stride * CB_T) != 0 || s + stride >= s_hi) return;
+  list[atomicAdd(cnt, 1u)] = (uint32_t)s;
+}
+
 __device__ __forceinline__ void emit_run(uint32_t* bstart, uint32_t* segpart, uint32_t b, uint64_t rs,
                                          const uint32_t* offsets, uint64_t seg, const g1_xyzz& acc) {
   if (rs == offsets[b])
@@ -371,6 +385,7 @@ __device__ __forceinline__ void emit_run(uint32_t* bstart, uint32_t* segpart, ui
 #endif
 __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __restrict__ bstart, uint32_t* __restrict__ segpart,
                                                     uint32_t* __restrict__ segowner,
+                                                    uint32_t* __restrict__ chunklist, uint32_t* __restrict__ chunkcnt,
                                                     const uint32_t* __restrict__ sorted,
                                                     const uint32_t* __restrict__ offsets, uint32_t nbins,
                                                     const uint32_t* __restrict__ table, uint32_t L) {
@@ -387,6 +402,7 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
   }
   uint32_t b = lo;
   segowner[s] = b;  // bucket of the segment's first run (read by the combine levels)
+  combine_enqueue(chunklist, chunkcnt, s, offsets[b], offsets[b + 1], L, 1);
   uint64_t rs = start;
   uint64_t bend = offsets[b + 1];
   g1_xyzz acc = g1_xyzz::inf();
@@ -419,9 +435,6 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
 // follow it (in place). The final pass then has <= ceil(m / CB_T^CB_LEVELS) partials per bucket, two
 // lanes per bucket joined by one xor-shuffle add. Depth for m partials: ~CB_T*CB_LEVELS + m/CB_T^3.
 // Lists of <= CB_T partials (every bucket of a uniform scalar distribution) skip the levels.
-constexpr uint32_t CB_T = 16;
-constexpr int CB_LEVELS = 3;
-
 __device__ __forceinline__ g1_xyzz shfl_xor_pt(const g1_xyzz& a, int mask) {
   g1_xyzz r;
 #pragma unroll
@@ -434,24 +447,26 @@ __device__ __forceinline__ g1_xyzz shfl_xor_pt(const g1_xyzz& a, int mask) {
   return r;
 }
 
+// level j: one thread per listed chunk start s (stride CB_T^j): add the CB_T - 1 partials that follow
+// at that stride, store in place, and list s for level j + 1 if it starts a chunk there
 __global__ void __launch_bounds__(256) k_combine_level(uint32_t* __restrict__ segpart,
                                                        const uint32_t* __restrict__ segowner,
-                                                       const uint32_t* __restrict__ offsets, uint32_t nbins,
+                                                       const uint32_t* __restrict__ offsets,
+                                                       const uint32_t* __restrict__ list_in,
+                                                       const uint32_t* __restrict__ cnt_in,
+                                                       uint32_t* __restrict__ list_out, uint32_t* __restrict__ cnt_out,
                                                        uint32_t L, uint64_t stride) {
-  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t E = offsets[nbins];
-  if (s * L >= E) return;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= *cnt_in) return;
+  const uint64_t s = list_in[t];
   const uint32_t b = segowner[s];
   const uint64_t o0 = offsets[b], o1 = offsets[b + 1];
-  if (s * L <= o0) return;  // this segment's first run starts its bucket (bstart), not a partial
-  const uint64_t s_lo = o0 / L + 1, s_hi = (o1 + L - 1) / L;  // partials [s_lo, s_hi)
-  if (s_hi - s_lo <= CB_T) return;  // short lists are summed directly by k_combine
-  if ((s - s_lo) % (stride * CB_T) != 0) return;
+  const uint64_t s_hi = (o1 + L - 1) / L;
   const uint64_t top = s + stride * CB_T < s_hi ? s + stride * CB_T : s_hi;
-  if (s + stride >= top) return;  // nothing to add
   g1_xyzz acc = g1_xyzz::load(segpart + 32 * s);
-  for (uint64_t t = s + stride; t < top; t += stride) acc.add(g1_xyzz::load(segpart + 32 * t));
+  for (uint64_t u = s + stride; u < top; u += stride) acc.add(g1_xyzz::load(segpart + 32 * u));
   acc.store(segpart + 32 * s);
+  if (list_out) combine_enqueue(list_out, cnt_out, s, o0, o1, L, stride * CB_T);
 }
 
 __global__ void __launch_bounds__(256) k_combine(uint32_t* __restrict__ buckets, const uint32_t* __restrict__ bstart,
@@ -578,13 +593,21 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   if (L < 4) L = 4;
   if (L > 64) L = 64;
   const uint64_t nseg = (E + L - 1) / L;
-  hipLaunchKernelGGL(k_accumulate, dim3(nb(nseg)), dim3(256), 0, st, w.bstart, w.segpart, w.segowner, w.sorted,
-                     w.offsets, B + 1, tb.table, (uint32_t)L);
+  // chunk lists of the combine levels: list j holds <= nseg / CB_T^(j+1) + B entries
+  uint32_t* cnt = w.chunkcnt;
+  const uint64_t lcap = nseg / CB_T + B + 16;
+  hipMemsetAsync(cnt, 0, 4 * CB_LEVELS, st);
+  hipLaunchKernelGGL(k_accumulate, dim3(nb(nseg)), dim3(256), 0, st, w.bstart, w.segpart, w.segowner, w.chunklist,
+                     cnt, w.sorted, w.offsets, B + 1, tb.table, (uint32_t)L);
   if (ev) hipEventRecord(ev[2], st);
-  uint64_t stride = 1;
-  for (int j = 0; j < CB_LEVELS; j++, stride *= CB_T)
-    hipLaunchKernelGGL(k_combine_level, dim3(nb(nseg)), dim3(256), 0, st, w.segpart, w.segowner, w.offsets, B + 1,
-                       (uint32_t)L, stride);
+  uint64_t stride = 1, cap = lcap;
+  for (int j = 0; j < CB_LEVELS; j++, stride *= CB_T) {
+    uint32_t* lin = w.chunklist + (uint64_t)j * lcap;
+    uint32_t* lout = j + 1 < CB_LEVELS ? w.chunklist + (uint64_t)(j + 1) * lcap : nullptr;
+    hipLaunchKernelGGL(k_combine_level, dim3(nb(cap)), dim3(256), 0, st, w.segpart, w.segowner, w.offsets, lin,
+                       cnt + j, lout, lout ? cnt + j + 1 : nullptr, (uint32_t)L, stride);
+    cap = cap / CB_T + B + 16;
+  }
   hipLaunchKernelGGL(k_combine, dim3(nb(2 * (uint64_t)B)), dim3(256), 0, st, w.buckets, w.bstart, w.segpart,
                      w.offsets, B, (uint32_t)L, stride);
   if (ev) hipEventRecord(ev[3], st);
