@@ -1,16 +1,18 @@
 // The reference's own test cases (test/mset_eq_kzg_grandsum.test.js:24-104 and the grand-product
 // twin) driven through the drop-in modules, without mocha: random inputs via curve.Fr.random, T = F
-// rotated by one, selectors ones except selF[n-1] = selT[0] = 0. Checks the proof shape; the
-// pairing verification of these proofs is done by tests/test_js_dropin.py with the oracle verifier.
+// rotated by one, selectors ones except selF[n-1] = selT[0] = 0. Like the reference's tests, every
+// proof must pass the verifier (here the drop-in verifier module: native transcript replay + pairing).
 const path = require("path");
-const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_grandproduct_prover } = require("../index");
+const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_grandproduct_prover,
+    mset_eq_kzg_grandsum_verifier, mset_eq_kzg_grandproduct_verifier } = require("../index");
 
 async function main() {
     const ptau = process.argv[2] || path.join("tmp", "powersOfTau28_hez_final_11.ptau");
     const curve = await getCurveFromName("bn128");
     const Fr = curve.Fr;
     let pass = 0;
-    for (const [name, fn, sname] of [["grandsum", mset_eq_kzg_grandsum_prover, "S"], ["grandproduct", mset_eq_kzg_grandproduct_prover, "Z"]]) {
+    for (const [name, fn, sname, vf] of [["grandsum", mset_eq_kzg_grandsum_prover, "S", mset_eq_kzg_grandsum_verifier],
+                                         ["grandproduct", mset_eq_kzg_grandproduct_prover, "Z", mset_eq_kzg_grandproduct_verifier]]) {
         for (const [nPols, sel] of [[1, false], [3, false], [1, true], [2, true]]) {
             const nBits = 1 + Math.floor(Math.random() * 6);
             const mk = () => {
@@ -34,6 +36,8 @@ async function main() {
             if (!keys.includes(sname) || !keys.includes("Q") || !keys.includes("Wxi") || !keys.includes("Wxiw"))
                 throw new Error(`${name}: bad proof keys ${keys}`);
             if (sel !== keys.includes("selF")) throw new Error("selector commitments mismatch");
+            const isValid = await vf(ptau, proof, nBits);  // test/mset_eq_kzg_grandsum.test.js: assert(isValid)
+            if (isValid !== true) throw new Error(`${name} nPols=${nPols} sel=${sel} nBits=${nBits}: proof rejected`);
             pass++;
         }
     }
