@@ -18,6 +18,7 @@ N > 1 GPUs (torchrun, one process per GPU): every rank proves its own independen
 
 Extra fields in the JSON line:
   proof_verified : one proof of the timed workload checked with the native verifier (pairing)
+  host_buffer_boundary : PCIe-inclusive latency of kgs_prove on pageable host buffers (the drop-in path)
   latency_ms_single_proof / round_ms_single_proof : one proof at a time on one context (2 MSM lanes)
   msm       : live HIP-event timing of the MSM phases at N = n (points/s, G1 adds/s)
   roofline  : the dominant kernel (MSM bucket accumulation, k_accumulate) against the INT-VALU
@@ -284,6 +285,33 @@ def main():
     value = total_proofs / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
+    # ---------------- host-buffer boundary (what the JS / Python drop-in modules call): kgs_prove on
+    # pageable host buffers, including the H2D copy of F/T and the D2H Montgomery write-back
+    host_leg = None
+    if rank == 0:
+        hf = [synth_evals(n, 1000 * rank + i)[0].tobytes() for i in range(args.npols)]
+        ht = [synth_evals(n, 1000 * rank + i)[1].tobytes() for i in range(args.npols)]
+        ctx.prove(kind, nbits, hf, ht)  # warm
+        t1 = time.perf_counter()
+        for _ in range(3):
+            ctx.prove(kind, nbits, hf, ht)
+        el = (time.perf_counter() - t1) / 3
+        host_leg = {"ms_per_proof": round(1000.0 * el, 3), "proofs_per_s": round(1.0 / el, 3),
+                    "note": "single context, one proof at a time; F/T in pageable host memory, Montgomery forms written back (prover.js:147-148)"}
+
+        # the JavaScript drop-in module itself (north star: JS host -> N-API -> libkgs), if node and
+        # the addon are present: best of 5 proofs, fresh inputs each, last proof verified
+        import shutil
+        import subprocess
+        js_dir = os.path.join(HERE, "kzg-grandsums-study_amd", "js")
+        if shutil.which("node") and os.path.exists(os.path.join(js_dir, "build", "kgs_addon.node")):
+            try:
+                out = subprocess.run(["node", os.path.join(js_dir, "test", "time_prove.js"), ptau, str(nbits), "5"],
+                                     capture_output=True, text=True, timeout=300)
+                host_leg["javascript_module"] = json.loads(out.stdout.strip().splitlines()[-1])
+            except Exception as e:  # the JS leg must not hide the GPU number
+                host_leg["javascript_module"] = {"error": str(e)[:200]}
+
     # ---------------- extra configs (BASELINE.json configs[2] and [4]), outside the timed region
     extra_cfg = {}
     if args.extra_legs:
@@ -401,6 +429,7 @@ def main():
                    "srs_power": power, "srs_points_resident": npts, "srs_gen_s": round(t_gen, 2),
                    "srs_load_s": round(t_load, 2)},
         "proof_verified": proof_verified,
+        "host_buffer_boundary": host_leg,
         "latency_ms_single_proof": round(latency_ms, 3),
         "round_ms_single_proof": [round(x, 3) for x in rounds],
         "msm": msm,

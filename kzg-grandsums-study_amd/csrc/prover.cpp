@@ -22,6 +22,8 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <functional>
+#include <thread>
 #include <vector>
 
 #include "../../include/kgs.h"
@@ -74,6 +76,9 @@ struct kgs_ctx {
   int device = 0;
   hipStream_t st = nullptr;
   std::map<std::string, DBuf> pool;
+  // pinned staging of the host-buffer boundary (kgs_prove's inputs and Montgomery write-back)
+  uint8_t* h_io = nullptr;
+  size_t h_io_bytes = 0;
   // pinned staging
   uint8_t* h_pin = nullptr;
   size_t h_pin_bytes = 0;
@@ -91,7 +96,8 @@ struct kgs_ctx {
   // between st and st2 (own work buffers), so one MSM's latency-bound tail overlaps the other's
   // bucket accumulation
   hipStream_t st2 = nullptr;
-  hipEvent_t ev_fork = nullptr;
+  hipStream_t st_copy = nullptr;  // Montgomery write-back of the host-buffer boundary
+  hipEvent_t ev_fork = nullptr, ev_copy = nullptr;
   MsmWork mw2;
   int msm_lanes = 2;  // kgs_ctx_set_msm_lanes
   uint64_t msm_nseg_max = 0;
@@ -110,8 +116,12 @@ struct kgs_ctx {
     if (st) hipStreamSynchronize(st);
     for (auto& kv : pool) hipFree(kv.second.p);
     if (h_pin) hipHostFree(h_pin);
+    if (h_io) hipHostFree(h_io);
     if (st2) hipStreamSynchronize(st2);
+    if (st_copy) hipStreamSynchronize(st_copy);
     if (ev_fork) hipEventDestroy(ev_fork);
+    if (ev_copy) hipEventDestroy(ev_copy);
+    if (st_copy) hipStreamDestroy(st_copy);
     if (st2) hipStreamDestroy(st2);
     if (st) hipStreamDestroy(st);
   }
@@ -128,6 +138,18 @@ struct kgs_ctx {
       b.bytes = bytes < 64 ? 64 : bytes;
     }
     return (uint32_t*)b.p;
+  }
+  uint8_t* io(size_t bytes) {
+    if (h_io_bytes < bytes) {
+      if (h_io) {
+        sync();
+        HC(hipHostFree(h_io));
+        h_io = nullptr;
+      }
+      HC(hipHostMalloc((void**)&h_io, bytes, hipHostMallocDefault));
+      h_io_bytes = bytes;
+    }
+    return h_io;
   }
   void ensure_pin(size_t bytes) {
     if (h_pin_bytes >= bytes) return;
@@ -160,6 +182,7 @@ struct kgs_ctx {
   void sync() {
     HC(hipStreamSynchronize(st));
     if (st2) HC(hipStreamSynchronize(st2));
+    if (st_copy) HC(hipStreamSynchronize(st_copy));
   }
   void reset_staging() {
     sync();
@@ -448,6 +471,7 @@ struct ProveIn {
   std::vector<const uint32_t*> f_std, t_std;  // device, standard form
   const uint32_t *sel_f = nullptr, *sel_t = nullptr;  // device, Montgomery (nullptr: unselected)
   std::vector<uint8_t*> mont_f_out, mont_t_out;  // host outputs (may be empty)
+  std::function<void()> after_round1;             // called once round 1 is synchronised
 };
 
 void set_lc_term(LinComb& lc, const uint32_t* src, uint64_t len, const Fr& coef) {
@@ -498,9 +522,17 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     intt_nat(c, Tc[i], tm[i], nbits);
   }
   check_launch();
-  for (int i = 0; i < k; i++) {
-    if (!in.mont_f_out.empty() && in.mont_f_out[i]) HC(hipMemcpyAsync(in.mont_f_out[i], fm[i], E, hipMemcpyDeviceToHost, c.st));
-    if (!in.mont_t_out.empty() && in.mont_t_out[i]) HC(hipMemcpyAsync(in.mont_t_out[i], tm[i], E, hipMemcpyDeviceToHost, c.st));
+  // Montgomery write-back (prover.js:147-148) on the copy stream, overlapping round 1's MSMs;
+  // fm/tm are not written again before the round-1 sync
+  bool wb = false;
+  for (int i = 0; i < k; i++) wb |= !in.mont_f_out.empty() && (in.mont_f_out[i] || in.mont_t_out[i]);
+  if (wb) {
+    HC(hipEventRecord(c.ev_copy, c.st));
+    HC(hipStreamWaitEvent(c.st_copy, c.ev_copy, 0));
+    for (int i = 0; i < k; i++) {
+      if (in.mont_f_out[i]) HC(hipMemcpyAsync(in.mont_f_out[i], fm[i], E, hipMemcpyDeviceToHost, c.st_copy));
+      if (in.mont_t_out[i]) HC(hipMemcpyAsync(in.mont_t_out[i], tm[i], E, hipMemcpyDeviceToHost, c.st_copy));
+    }
   }
   uint32_t *sFc = nullptr, *sTc = nullptr;
   if (sel) {
@@ -521,6 +553,7 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     r1.push_back(commit_launch(c, sTc, n, slot++, 1));
   }
   c.sync();
+  if (in.after_round1) in.after_round1();
   const int ncom = 2 * k + (sel ? 2 : 0) + 4;
   std::vector<std::vector<uint8_t>> com(ncom, std::vector<uint8_t>(64));
   int ci = 0;
@@ -874,6 +907,8 @@ int kgs_ctx_create(int device, kgs_ctx_t** out) {
     HC(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     HC(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
     HC(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    HC(hipStreamCreateWithFlags(&c->st_copy, hipStreamNonBlocking));
+    HC(hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming));
     c->d_scal = c->buf("scalars", kgs_ctx::SCAL_BYTES);
     c->ensure_pin(8 << 20);
     *out = c;
@@ -1032,6 +1067,34 @@ int kgs_proof_shape(int kind, int npols, int selected, int* n_commitments, int* 
   return KGS_OK;
 }
 
+namespace {
+// host copies between pageable caller buffers and the pinned staging area, split over threads
+struct CopyJob {
+  uint8_t* dst;
+  const uint8_t* src;
+  size_t len;
+};
+void par_copy(const std::vector<CopyJob>& jobs) {
+  const size_t piece = 1u << 20;
+  std::vector<CopyJob> pieces;
+  for (const auto& j : jobs)
+    for (size_t o = 0; o < j.len; o += piece) pieces.push_back({j.dst + o, j.src + o, std::min(piece, j.len - o)});
+  unsigned nth = std::thread::hardware_concurrency();
+  nth = std::max(1u, std::min(nth, 16u));
+  if (pieces.size() < 2 || nth == 1) {
+    for (const auto& p : pieces) memcpy(p.dst, p.src, p.len);
+    return;
+  }
+  nth = std::min<unsigned>(nth, (unsigned)pieces.size());
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nth; t++)
+    th.emplace_back([&, t] {
+      for (size_t i = t; i < pieces.size(); i += nth) memcpy(pieces[i].dst, pieces[i].src, pieces[i].len);
+    });
+  for (auto& x : th) x.join();
+}
+}  // namespace
+
 int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* const* evals_f,
               const uint8_t* const* evals_t, const uint8_t* sel_f, const uint8_t* sel_t, uint8_t* const* mont_f,
               uint8_t* const* mont_t, uint8_t* commitments_out, uint8_t* evaluations_out) {
@@ -1046,25 +1109,59 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   in.kind = kind;
   in.nbits = nbits;
   in.npols = npols;
+  // pageable caller buffers -> pinned staging (parallel host copies) -> one DMA per vector; the
+  // Montgomery write-back goes device -> the same pinned slots -> caller (after the proof)
+  const int nvec = 2 * npols + (sel_f ? 2 : 0);
+  uint8_t* pio = ctx->io((size_t)nvec * E);
+  std::vector<CopyJob> in_jobs;
   for (int i = 0; i < npols; i++) {
-    uint32_t* df = ctx->buf("in_f" + std::to_string(i), E);
-    uint32_t* dt = ctx->buf("in_t" + std::to_string(i), E);
-    HC(hipMemcpyAsync(df, evals_f[i], E, hipMemcpyHostToDevice, ctx->st));
-    HC(hipMemcpyAsync(dt, evals_t[i], E, hipMemcpyHostToDevice, ctx->st));
-    in.f_std.push_back(df);
-    in.t_std.push_back(dt);
-    in.mont_f_out.push_back(mont_f ? mont_f[i] : nullptr);
-    in.mont_t_out.push_back(mont_t ? mont_t[i] : nullptr);
+    in_jobs.push_back({pio + (size_t)(2 * i) * E, evals_f[i], E});
+    in_jobs.push_back({pio + (size_t)(2 * i + 1) * E, evals_t[i], E});
   }
   if (sel_f) {
-    uint32_t* a = ctx->buf("in_sf", E);
-    uint32_t* b = ctx->buf("in_st", E);
-    HC(hipMemcpyAsync(a, sel_f, E, hipMemcpyHostToDevice, ctx->st));
-    HC(hipMemcpyAsync(b, sel_t, E, hipMemcpyHostToDevice, ctx->st));
-    in.sel_f = a;
-    in.sel_t = b;
+    in_jobs.push_back({pio + (size_t)(2 * npols) * E, sel_f, E});
+    in_jobs.push_back({pio + (size_t)(2 * npols + 1) * E, sel_t, E});
   }
-  prove_impl(*ctx, in, commitments_out, evaluations_out);
+  ctx->sync();  // the staging area may still feed a previous call's copies
+  // inputs: one parallel host copy into the pinned slots, then one DMA per vector
+  std::vector<uint32_t*> dsts;
+  for (int i = 0; i < npols; i++) {
+    dsts.push_back(ctx->buf("in_f" + std::to_string(i), E));
+    dsts.push_back(ctx->buf("in_t" + std::to_string(i), E));
+  }
+  if (sel_f) {
+    dsts.push_back(ctx->buf("in_sf", E));
+    dsts.push_back(ctx->buf("in_st", E));
+  }
+  par_copy(in_jobs);
+  for (size_t v = 0; v < in_jobs.size(); v++)
+    HC(hipMemcpyAsync(dsts[v], in_jobs[v].dst, E, hipMemcpyHostToDevice, ctx->st));
+  for (int i = 0; i < npols; i++) {
+    in.f_std.push_back(dsts[2 * i]);
+    in.t_std.push_back(dsts[2 * i + 1]);
+    in.mont_f_out.push_back(mont_f && mont_f[i] ? pio + (size_t)(2 * i) * E : nullptr);
+    in.mont_t_out.push_back(mont_t && mont_t[i] ? pio + (size_t)(2 * i + 1) * E : nullptr);
+  }
+  if (sel_f) {
+    in.sel_f = dsts[2 * npols];
+    in.sel_t = dsts[2 * npols + 1];
+  }
+  // the Montgomery forms are in the pinned slots once round 1 is synchronised: copy them to the
+  // caller on a host thread while rounds 2-5 run
+  std::vector<CopyJob> out_jobs;
+  for (int i = 0; i < npols; i++) {
+    if (mont_f && mont_f[i]) out_jobs.push_back({mont_f[i], pio + (size_t)(2 * i) * E, E});
+    if (mont_t && mont_t[i]) out_jobs.push_back({mont_t[i], pio + (size_t)(2 * i + 1) * E, E});
+  }
+  struct Joiner {
+    std::thread t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } out_copy;
+  if (!out_jobs.empty()) in.after_round1 = [&] { out_copy.t = std::thread([&] { par_copy(out_jobs); }); };
+  prove_impl(*ctx, in, commitments_out, evaluations_out);  // ends synchronised
+  if (out_copy.t.joinable()) out_copy.t.join();
   API_END
 }
 

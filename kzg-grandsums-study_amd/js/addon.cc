@@ -3,6 +3,7 @@
 // return Promises, like the reference's async module API.
 #include <node_api.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <string>
 #include <vector>
@@ -46,6 +47,54 @@ static std::vector<uint8_t> bytes_of(napi_env env, napi_value v) {
     out.assign((uint8_t*)data, (uint8_t*)data + len);
   }
   return out;
+}
+
+// zero-copy view of a Uint8Array / Buffer argument, kept alive by a reference until the async
+// work completes (ArrayBuffer backing stores do not move)
+struct View {
+  const uint8_t* p = nullptr;
+  size_t len = 0;
+};
+static View view_of(napi_env env, napi_value v, std::vector<napi_ref>& refs) {
+  View out;
+  bool is_ta = false;
+  napi_is_typedarray(env, v, &is_ta);
+  if (is_ta) {
+    napi_typedarray_type t;
+    size_t len;
+    void* data;
+    napi_value ab;
+    size_t off;
+    napi_get_typedarray_info(env, v, &t, &len, &data, &ab, &off);
+    out.p = (const uint8_t*)data;
+    out.len = len;
+  } else {
+    bool is_buf = false;
+    napi_is_buffer(env, v, &is_buf);
+    if (is_buf) {
+      void* data;
+      size_t len;
+      napi_get_buffer_info(env, v, &data, &len);
+      out.p = (const uint8_t*)data;
+      out.len = len;
+    }
+  }
+  napi_ref r;
+  if (napi_create_reference(env, v, 1, &r) == napi_ok) refs.push_back(r);
+  return out;
+}
+
+static void free_finalize(napi_env, void* data, void*) { free(data); }
+
+// Uint8Array over a malloc'd buffer handed to JS without a copy (freed by the GC finalizer)
+static napi_value adopt_u8(napi_env env, uint8_t* data, size_t len) {
+  napi_value ab, ta;
+  if (napi_create_external_arraybuffer(env, data, len, free_finalize, nullptr, &ab) != napi_ok) {
+    free(data);
+    return nullptr;
+  }
+  napi_create_typedarray(env, napi_uint8_array, len, ab, 0, &ta);
+  return ta;
 }
 
 static napi_value make_u8(napi_env env, const uint8_t* data, size_t len) {
@@ -122,8 +171,11 @@ struct Job {
   int nbits_max = -1;
   // prove
   int kind = 0, nbits = 0, npols = 0;
-  std::vector<std::vector<uint8_t>> f, t, mf, mt;
-  std::vector<uint8_t> sf, st, com, ev;
+  std::vector<View> f, t;
+  View sf, st;
+  std::vector<uint8_t*> mf, mt;  // malloc'd, adopted by JS on success
+  std::vector<uint8_t> com, ev;
+  std::vector<napi_ref> refs;
   bool selected = false;
 };
 
@@ -137,18 +189,24 @@ static void job_execute(napi_env, void* data) {
     j->com.resize(64 * (size_t)nc);
     j->ev.resize(32 * (size_t)ne);
     std::vector<const uint8_t*> fp, tp;
-    std::vector<uint8_t*> mfp, mtp;
     const size_t E = (size_t)32 << j->nbits;
-    j->mf.assign(j->npols, std::vector<uint8_t>(E));
-    j->mt.assign(j->npols, std::vector<uint8_t>(E));
+    bool ok = true;
     for (int i = 0; i < j->npols; i++) {
-      fp.push_back(j->f[i].data());
-      tp.push_back(j->t[i].data());
-      mfp.push_back(j->mf[i].data());
-      mtp.push_back(j->mt[i].data());
+      ok &= j->f[i].len == E && j->t[i].len == E;
+      fp.push_back(j->f[i].p);
+      tp.push_back(j->t[i].p);
+      j->mf.push_back((uint8_t*)malloc(E));
+      j->mt.push_back((uint8_t*)malloc(E));
+      ok &= j->mf.back() && j->mt.back();
     }
-    j->rc = kgs_prove(j->ctx, j->kind, j->nbits, j->npols, fp.data(), tp.data(), j->selected ? j->sf.data() : nullptr,
-                      j->selected ? j->st.data() : nullptr, mfp.data(), mtp.data(), j->com.data(), j->ev.data());
+    if (j->selected) ok &= j->sf.len == E && j->st.len == E;
+    if (!ok) {
+      j->rc = KGS_E_ARG;
+      j->err = "evaluation buffers must hold 2^nbits 32-byte elements";
+      return;
+    }
+    j->rc = kgs_prove(j->ctx, j->kind, j->nbits, j->npols, fp.data(), tp.data(), j->selected ? j->sf.p : nullptr,
+                      j->selected ? j->st.p : nullptr, j->mf.data(), j->mt.data(), j->com.data(), j->ev.data());
   }
   if (j->rc != KGS_OK) j->err = kgs_last_error();
 }
@@ -176,13 +234,19 @@ static void job_complete(napi_env env, napi_status, void* data) {
     for (size_t i = 0; i < j->ev.size() / 32; i++) napi_set_element(env, arr, (uint32_t)i, make_u8(env, &j->ev[32 * i], 32));
     napi_set_named_property(env, o, "evaluations", arr);
     napi_create_array(env, &arr);
-    for (size_t i = 0; i < j->mf.size(); i++) napi_set_element(env, arr, (uint32_t)i, make_u8(env, j->mf[i].data(), j->mf[i].size()));
+    const size_t E = (size_t)32 << j->nbits;
+    for (size_t i = 0; i < j->mf.size(); i++) napi_set_element(env, arr, (uint32_t)i, adopt_u8(env, j->mf[i], E));
     napi_set_named_property(env, o, "montF", arr);
     napi_create_array(env, &arr);
-    for (size_t i = 0; i < j->mt.size(); i++) napi_set_element(env, arr, (uint32_t)i, make_u8(env, j->mt[i].data(), j->mt[i].size()));
+    for (size_t i = 0; i < j->mt.size(); i++) napi_set_element(env, arr, (uint32_t)i, adopt_u8(env, j->mt[i], E));
     napi_set_named_property(env, o, "montT", arr);
+    j->mf.clear();
+    j->mt.clear();
     napi_resolve_deferred(env, j->deferred, o);
   }
+  for (uint8_t* p : j->mf) free(p);  // error path: not adopted
+  for (uint8_t* p : j->mt) free(p);
+  for (napi_ref r : j->refs) napi_delete_reference(env, r);
   napi_delete_async_work(env, j->work);
   delete j;
 }
@@ -230,16 +294,16 @@ static napi_value Prove(napi_env env, napi_callback_info info) {
   for (uint32_t i = 0; i < nf; i++) {
     napi_value e;
     napi_get_element(env, argv[3], i, &e);
-    j->f.push_back(bytes_of(env, e));
+    j->f.push_back(view_of(env, e, j->refs));
     napi_get_element(env, argv[4], i, &e);
-    j->t.push_back(bytes_of(env, e));
+    j->t.push_back(view_of(env, e, j->refs));
   }
   napi_valuetype ty;
   napi_typeof(env, argv[5], &ty);
   if (ty != napi_null && ty != napi_undefined) {
     j->selected = true;
-    j->sf = bytes_of(env, argv[5]);
-    j->st = bytes_of(env, argv[6]);
+    j->sf = view_of(env, argv[5], j->refs);
+    j->st = view_of(env, argv[6], j->refs);
   }
   return queue(env, j, "kgs_prove");
 }

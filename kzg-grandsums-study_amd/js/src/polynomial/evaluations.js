@@ -16,8 +16,12 @@ class Evaluations {
     }
     static fromEvals(evals) { return new Evaluations(evals.eval.slice(), evals.curve); }
     static getOneEvals(length, curve) {
-        const buffer = new Uint8Array(length * curve.Fr.n8);
-        for (let i = 0; i < length; i++) buffer.set(curve.Fr.one, i * curve.Fr.n8);
+        const n8 = curve.Fr.n8, buffer = new Uint8Array(length * n8);
+        if (length > 0) {
+            buffer.set(curve.Fr.one, 0);
+            for (let filled = n8; filled < buffer.length; filled *= 2)  // doubling copies (memcpy)
+                buffer.copyWithin(filled, 0, Math.min(filled, buffer.length - filled));
+        }
         return new Evaluations(buffer, curve);
     }
     static getZeroEvals(length, curve) { return new Evaluations(new Uint8Array(length * curve.Fr.n8), curve); }
@@ -52,10 +56,21 @@ class Evaluations {
     }
     isEqual(other) {
         if (this.length() !== other.length()) return false;
-        return Buffer.compare(Buffer.from(this.eval), Buffer.from(other.eval)) === 0;
+        return Buffer.compare(view(this.eval), view(other.eval)) === 0;
     }
-    isAllZeros() { return this.isEqual(new Evaluations(new Uint8Array(this.length() * this.Fr.n8), this.curve)); }
-    isAllOnes() { return this.isEqual(Evaluations.getOneEvals(this.length(), this.curve)); }
+    // every element equals the first one: element 0 matches, and the vector equals itself shifted by
+    // one element (one native compare, no second vector)
+    isConstant(value) {
+        const n8 = this.Fr.n8, b = view(this.eval);
+        if (b.length === 0) return true;
+        if (Buffer.compare(b.subarray(0, n8), view(value)) !== 0) return false;
+        return Buffer.compare(b.subarray(n8), b.subarray(0, b.length - n8)) === 0;
+    }
+    isAllZeros() { return this.isConstant(this.Fr.zero); }
+    isAllOnes() { return this.isConstant(this.Fr.one); }
 }
+
+// Buffer over a Uint8Array's memory (no copy, unlike Buffer.from(typedArray))
+function view(u8) { return Buffer.from(u8.buffer, u8.byteOffset, u8.byteLength); }
 
 module.exports = { Evaluations };

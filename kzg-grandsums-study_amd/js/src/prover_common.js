@@ -19,15 +19,23 @@ async function prove(kind, pTauFilename, evalsFs, evalsTs, evalsSelF, evalsSelT)
             throw new Error("The multiset buffers must all have the same length.");
         }
     }
-    if (evalsSelF === null || evalsSelF === undefined) evalsSelF = Evaluations.getOneEvals(evalsFs[0].length(), curve);
-    if (evalsSelT === null || evalsSelT === undefined) evalsSelT = Evaluations.getOneEvals(evalsTs[0].length(), curve);
-    if (evalsSelF.length() !== evalsSelT.length()) {
+    // absent selectors are all-ones vectors in the reference (prover.js:53-68): unselected, so they
+    // need not be materialised; given ones are checked with the same rules and messages
+    const noSelF = evalsSelF === null || evalsSelF === undefined;
+    const noSelT = evalsSelT === null || evalsSelT === undefined;
+    const lenSelF = noSelF ? evalsFs[0].length() : evalsSelF.length();
+    const lenSelT = noSelT ? evalsTs[0].length() : evalsSelT.length();
+    if (lenSelF !== lenSelT) {
         throw new Error("The selection buffers must have the same length.");
-    } else if (evalsSelF.length() !== evalsFs[0].length()) {
+    } else if (lenSelF !== evalsFs[0].length()) {
         throw new Error("The selection buffers must have the same length as the multiset buffers.");
     }
     let isSelected = true;
-    if (evalsSelF.isAllOnes() && evalsSelT.isAllOnes()) isSelected = false;
+    if ((noSelF || evalsSelF.isAllOnes()) && (noSelT || evalsSelT.isAllOnes())) isSelected = false;
+    if (isSelected) {
+        if (noSelF) evalsSelF = Evaluations.getOneEvals(lenSelF, curve);
+        if (noSelT) evalsSelT = Evaluations.getOneEvals(lenSelT, curve);
+    }
     const nBits = Math.ceil(Math.log2(evalsFs[0].length()));
     if (evalsFs[0].length() !== 2 ** nBits) throw new Error("Polynomial length must be a power of two.");
     const ctx = await backend.context(0);
