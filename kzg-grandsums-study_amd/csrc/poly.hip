@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(1024) k_tile_inverse(uint32_t* __restrict__ ti
     __syncthreads();
   }
   if (t == 1023) {
-    fr total_inv = pre.inverse();
+    fr total_inv = pre.inverse_bgcd();  // one lane: binary Euclid (~5x fewer instructions than Fermat)
     total_inv.store(tot);
   }
   __syncthreads();
