@@ -341,6 +341,11 @@ void shard_range(uint64_t n, int rank, int world, uint64_t& lo, uint64_t& hi) {
 
 // the second MSM lane starts after everything issued so far on the main stream (the round's inputs)
 void fork_lanes(kgs_ctx& c) {
+  if (c.msm_lanes < 2) return;
+  if (!c.st2) {
+    HC(hipStreamCreateWithFlags(&c.st2, hipStreamNonBlocking));
+    HC(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
+  }
   HC(hipEventRecord(c.ev_fork, c.st));
   HC(hipStreamWaitEvent(c.st2, c.ev_fork, 0));
 }
@@ -527,6 +532,10 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   bool wb = false;
   for (int i = 0; i < k; i++) wb |= !in.mont_f_out.empty() && (in.mont_f_out[i] || in.mont_t_out[i]);
   if (wb) {
+    if (!c.st_copy) {
+      HC(hipStreamCreateWithFlags(&c.st_copy, hipStreamNonBlocking));
+      HC(hipEventCreateWithFlags(&c.ev_copy, hipEventDisableTiming));
+    }
     HC(hipEventRecord(c.ev_copy, c.st));
     HC(hipStreamWaitEvent(c.st_copy, c.ev_copy, 0));
     for (int i = 0; i < k; i++) {
@@ -905,10 +914,8 @@ int kgs_ctx_create(int device, kgs_ctx_t** out) {
     auto* c = new kgs_ctx();
     c->device = device;
     HC(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-    HC(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
-    HC(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-    HC(hipStreamCreateWithFlags(&c->st_copy, hipStreamNonBlocking));
-    HC(hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming));
+    // the second MSM lane and the copy stream are created on first use: contexts that never need
+    // them keep one stream (several in-flight contexts share the device's few hardware queues)
     c->d_scal = c->buf("scalars", kgs_ctx::SCAL_BYTES);
     c->ensure_pin(8 << 20);
     *out = c;
