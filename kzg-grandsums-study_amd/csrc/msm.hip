@@ -133,6 +133,11 @@ __device__ __forceinline__ uint32_t wave_excl_scan256(const uint32_t* a, uint32_
 // partition of a nonzero digit magnitude: (key - 1) >> lob
 __device__ __forceinline__ uint32_t part_of(uint32_t key, int lob) { return (key - 1) >> lob; }
 
+#ifndef KGS_SORT_SPT
+#define KGS_SORT_SPT 2
+#endif
+constexpr int SORT_SPT = KGS_SORT_SPT;  // scalars per thread in the histogram / partition passes
+
 template <int C>
 __global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ bh, const uint32_t* __restrict__ sc,
                                                    uint64_t N, int lob, int NH, uint32_t nblk) {
@@ -141,13 +146,15 @@ __global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ bh, co
   __shared__ uint32_t h[256];
   h[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < N) {
-    int32_t d[W];
-    scalar_digits<C>(d, sc, i);
+  for (int q = 0; q < SORT_SPT; q++) {
+    const uint64_t i = ((uint64_t)blockIdx.x * SORT_SPT + q) * 256 + threadIdx.x;
+    if (i < N) {
+      int32_t d[W];
+      scalar_digits<C>(d, sc, i);
 #pragma unroll
-    for (int j = 0; j < W; j++) {
-      if (d[j]) atomicAdd(&h[part_of((uint32_t)(d[j] < 0 ? -d[j] : d[j]), lob)], 1u);
+      for (int j = 0; j < W; j++) {
+        if (d[j]) atomicAdd(&h[part_of((uint32_t)(d[j] < 0 ? -d[j] : d[j]), lob)], 1u);
+      }
     }
   }
   __syncthreads();
@@ -199,8 +206,8 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
                                                    uint64_t N, uint64_t Nsrs, int lob, int NH, uint32_t nblk) {
   constexpr int W = (255 + C - 1) / C;
   extern __shared__ uint32_t smem[];
-  uint32_t* sval = smem;                             // 256 * W
-  uint16_t* skey = (uint16_t*)(smem + 256 * W);      // 256 * W (key - 1 < 2^16)
+  uint32_t* sval = smem;                                        // 256 * SORT_SPT * W
+  uint16_t* skey = (uint16_t*)(smem + 256 * SORT_SPT * W);      // same count (key - 1 < 2^16)
   __shared__ uint32_t base[256], loff[256], cur[256];
   __shared__ uint32_t total;
   const uint32_t blk = blockIdx.x, tid = threadIdx.x;
@@ -218,17 +225,19 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
   __syncthreads();
   if ((int)tid < NH) cur[tid] = loff[tid];
   __syncthreads();
-  const uint64_t i = (uint64_t)blk * blockDim.x + tid;
-  if (i < N) {
-    int32_t d[W];
-    scalar_digits<C>(d, sc, i);
+  for (int q = 0; q < SORT_SPT; q++) {
+    const uint64_t i = ((uint64_t)blk * SORT_SPT + q) * 256 + tid;
+    if (i < N) {
+      int32_t d[W];
+      scalar_digits<C>(d, sc, i);
 #pragma unroll
-    for (int j = 0; j < W; j++) {
-      if (!d[j]) continue;
-      const uint32_t k = (uint32_t)(d[j] < 0 ? -d[j] : d[j]);
-      const uint32_t pos = atomicAdd(&cur[part_of(k, lob)], 1u);
-      sval[pos] = (uint32_t)((uint64_t)j * Nsrs + i) | (d[j] < 0 ? 0x80000000u : 0u);
-      skey[pos] = (uint16_t)(k - 1);
+      for (int j = 0; j < W; j++) {
+        if (!d[j]) continue;
+        const uint32_t k = (uint32_t)(d[j] < 0 ? -d[j] : d[j]);
+        const uint32_t pos = atomicAdd(&cur[part_of(k, lob)], 1u);
+        sval[pos] = (uint32_t)((uint64_t)j * Nsrs + i) | (d[j] < 0 ? 0x80000000u : 0u);
+        skey[pos] = (uint16_t)(k - 1);
+      }
     }
   }
   __syncthreads();
@@ -248,7 +257,10 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
 // Chunks keep a skewed partition (all points in one bucket: a selector polynomial's equal
 // coefficients) spread over SL_G workgroups instead of one.
 constexpr int SL_THREADS = 1024;
-constexpr int SL_TILE = 4096;
+#ifndef KGS_SL_TILE
+#define KGS_SL_TILE 4096
+#endif
+constexpr int SL_TILE = KGS_SL_TILE;
 constexpr int SL_G = 16;
 
 __device__ __forceinline__ void chunk_range(uint32_t s0, uint32_t s1, int g, uint32_t& c0, uint32_t& c1) {
@@ -563,11 +575,11 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   int lob = c - 1 < 7 ? c - 1 : 7;
   if (c - 9 > lob) lob = c - 9;
   const int NH = (int)(B >> lob);
-  const uint32_t nblk = (uint32_t)nb(N);
+  const uint32_t nblk = (uint32_t)((N + 256 * SORT_SPT - 1) / (256 * SORT_SPT));
   uint32_t* ptot = w.counts;           // NH partition totals
   uint32_t* hi_off = w.cursor;         // NH + 1
   uint32_t* bh = w.blockhist;          // NH x nblk
-  const size_t part_lds = (size_t)256 * W * 6;
+  const size_t part_lds = (size_t)256 * SORT_SPT * W * 6;
   switch (c) {
 #define KGS_SORT_C(CC)                                                                                         \
   case CC:                                                                                                      \
