@@ -615,7 +615,27 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
                  c.buf("bt_ti", 32 * (ntiles + 1)), flags);
   intt_nat(c, Sc, Sev, nbits);
   check_launch();
-  Commit cS = commit_launch(c, Sc, n, slot++);
+  // the S commitment runs on the second MSM lane while the main stream already computes round 3's
+  // challenge-independent coset evaluations of S, F, T (+ selectors)
+  fork_lanes(c);
+  Commit cS = commit_launch(c, Sc, n, slot++, 1);
+  const int lcs = (!gs && !sel) ? nbits : nbits + 1;
+  const uint64_t cs = 1ull << lcs;
+  uint32_t* cosS = c.buf("cosS", 32 * cs);
+  uint32_t* cosF = c.buf("cosF", 32 * cs);
+  uint32_t* cosT = c.buf("cosT", 32 * cs);
+  uint32_t *cosSF = nullptr, *cosST = nullptr;
+  coset_fwd(c, cosS, Sc, n, lcs);
+  coset_fwd(c, cosF, polF, n, lcs);
+  coset_fwd(c, cosT, polT, n, lcs);
+  if (sel) {
+    cosSF = c.buf("cosSF", 32 * cs);
+    cosST = c.buf("cosST", 32 * cs);
+    coset_fwd(c, cosSF, sFc, n, lcs);
+    coset_fwd(c, cosST, sTc, n, lcs);
+  }
+  uint32_t* nxm1 = get_nxm1(c, nbits, lcs);
+  check_launch();
   uint32_t* h_flags = (uint32_t*)c.pin(64);
   HC(hipMemcpyAsync(h_flags, flags, 64, hipMemcpyDeviceToHost, c.st));
   c.sync();
@@ -630,29 +650,13 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   tr.add_scalar(gamma);
   tr.add_commitment(com[iS].data());
   const Fr alpha = tr.challenge();
-  const int lcs = (!gs && !sel) ? nbits : nbits + 1;
-  const uint64_t cs = 1ull << lcs;
   const uint32_t rot = (uint32_t)(cs >> nbits);
   const uint64_t qlen = (!gs && !sel) ? n - 1 : 2 * n - 2;  // deg Q + 1 bound
   Fr gn = Fr::from_u64(5).pow_u64(n);
   Fr qs[4] = {alpha, gamma, (gn - Fr::one()).inverse(), (gn.neg() - Fr::one()).inverse()};
   uint32_t* d_qs = c.scal(qs, 4);
   launch_divcheck(c.st, !gs, sel, flags + 1, Sev, fcomb, tcomb, in.sel_f, in.sel_t, d_qs, n);
-  uint32_t* cosS = c.buf("cosS", 32 * cs);
-  uint32_t* cosF = c.buf("cosF", 32 * cs);
-  uint32_t* cosT = c.buf("cosT", 32 * cs);
-  uint32_t *cosSF = nullptr, *cosST = nullptr;
-  coset_fwd(c, cosS, Sc, n, lcs);
-  coset_fwd(c, cosF, polF, n, lcs);
-  coset_fwd(c, cosT, polT, n, lcs);
-  if (sel) {
-    cosSF = c.buf("cosSF", 32 * cs);
-    cosST = c.buf("cosST", 32 * cs);
-    coset_fwd(c, cosSF, sFc, n, lcs);
-    coset_fwd(c, cosST, sTc, n, lcs);
-  }
   uint32_t* Qc = c.buf("Qc", 32 * cs);
-  uint32_t* nxm1 = get_nxm1(c, nbits, lcs);
   launch_quotient(c.st, !gs, sel, Qc, cosS, cosF, cosT, cosSF, cosST, nxm1, d_qs, lcs, rot);
   coset_inv(c, Qc, Qc, lcs);
   check_launch();
