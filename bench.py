@@ -21,8 +21,9 @@ Extra fields in the JSON line:
   host_buffer_boundary : PCIe-inclusive latency of kgs_prove on pageable host buffers (the drop-in path)
   latency_ms_single_proof / round_ms_single_proof : one proof at a time on one context (2 MSM lanes)
   msm       : live HIP-event timing of the MSM phases at N = n (points/s, G1 adds/s)
-  roofline  : the dominant kernel (MSM bucket accumulation, k_accumulate) against the INT-VALU
-              Montgomery-product roof; traffic = PMC FETCH+WRITE from profiles/
+  roofline  : the dominant kernel (MSM bucket accumulation, k_accumulate) against the chip's
+              v_mad_u64_u32 issue rate (INT-VALU bound); traffic = PMC FETCH+WRITE
+              from profiles/
   hbm_view  : proof-level bytes (SURVEY.md §8d's count over the reference op list) per second vs 8 TB/s
   extra_configs : BASELINE.json configs[2] (grand-product at n), configs[3] (grand-sum n = 2^24) and
               configs[4] (selected-vector k = 4, n = 2^22) — single GPU at N = 1, every MSM
@@ -62,6 +63,10 @@ def synth_evals(n, idx):
 
 
 BENCH_TAU = None
+# v_mad_u64_u32 issue rate of the whole chip: 256 CUs x 4 SIMDs x 64 lanes / 4.97 cycles x 2.4 GHz
+# (measured: profiles/ubench/issue_rates.hip); one 9 x 29-bit Montgomery product issues 162
+MAD_PEAK = 256 * 4 * 64 / 4.97 * 2.4e9
+MADS_PER_PRODUCT = 162
 
 
 def bench_tau():
@@ -372,13 +377,15 @@ def main():
     }
 
     # ---------------- roofline of the dominant kernel (k_accumulate)
-    # algorithmic work per launch: entries x 1 mixed XYZZ add (madd-2008-s: 8M + 2S = 10 Fq
-    # Montgomery products). Peak: v_mad_u64_u32 issue bound, 19.66e12 /s (256 CU x 4 SIMD x 64 lanes /
-    # 8 cycles x 2.4 GHz) / 128 mads per 8x32-bit CIOS product = 153.6 G products/s.
+    # The kernel is integer-VALU issue bound. Algorithmic work per launch: entries x 1 mixed XYZZ add
+    # (madd-2008-s: 8M + 2S = 10 Fq Montgomery products) x 162 v_mad_u64_u32 per product (9 x 29-bit
+    # limbs, field29.hpp). Peak: the chip's measured v_mad_u64_u32 issue rate, MAD_PEAK (4.97 SIMD
+    # cycles per wave64 instruction at the 2.4 GHz nominal clock, profiles/ubench/ubench_r01.txt):
+    # frac = the share of the SIMDs' issue capacity spent on the product's multiply-adds.
     acc_ms = ph[1]
     mults = 10 * entries.value
-    achieved = mults / (acc_ms / 1e3) / 1e9
-    peak = 19.6608e12 / 128 / 1e9
+    achieved = mults * MADS_PER_PRODUCT / (acc_ms / 1e3) / 1e12
+    peak = MAD_PEAK / 1e12
     traffic = None
     pmc_path = os.path.join(HERE, "profiles", "pmc_accumulate.json")
     if os.path.exists(pmc_path):
@@ -387,8 +394,9 @@ def main():
                 traffic = json.load(fh).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    roofline = {"bound": "valu", "kernel": "k_accumulate", "achieved": round(achieved, 2), "peak": round(peak, 2),
-                "unit": "G Fq-mont-mul/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+    roofline = {"bound": "valu", "kernel": "k_accumulate", "achieved": round(achieved, 3), "peak": round(peak, 3),
+                "unit": "T v_mad_u64_u32/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                "fq_products_per_s": round(mults / (acc_ms / 1e3)), "g1_adds_per_s": round(entries.value / (acc_ms / 1e3)),
                 "algorithmic_bytes_per_launch": 68 * entries.value,
                 "hbm_gbps_algorithmic": round(68 * entries.value / (acc_ms / 1e3) / 1e9, 1)}
 

@@ -40,6 +40,7 @@ struct MsmWork {
   uint32_t* locnt = nullptr;     // lo pass: 256 partitions x 256 lo x 16 chunks counts / bases
   uint32_t* chunklist = nullptr; // combine levels: 3 lists of chunk-start segments
   uint32_t* chunkcnt = nullptr;  // their lengths
+  uint32_t* raw29 = nullptr;     // accumulate output in the fq29 form (B + 1 + nseg entries x 160 B)
 };
 
 // ntt.hip

@@ -14,6 +14,7 @@
 //  * sum_b b·S_b = sum_k 2^k T_k with T_k = sum_{b has bit k} S_b: c independent tree
 //    reductions (chip-parallel), then the c-term Horner + affine conversion on the host.
 #include "kernels.hpp"
+#include "field29.hpp"
 
 namespace kgs {
 
@@ -62,6 +63,16 @@ __global__ void __launch_bounds__(256) k_batch_affine(uint32_t* __restrict__ out
   }
 }
 
+// table coordinates x*2^256 -> x*2^261 (the fq29 Montgomery form of the bucket accumulation)
+__global__ void __launch_bounds__(256) k_tab_to29(uint32_t* __restrict__ table, uint64_t nelem) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nelem) return;
+  fq c;
+#pragma unroll
+  for (int k = 0; k < 8; k++) c.v[k] = f29::C261W[k];
+  (fq::load(table + 8 * i) * c).store(table + 8 * i);
+}
+
 void msm_build_table(hipStream_t st, uint32_t* table, uint64_t npts, int c, int W, uint32_t* tmp_xyzz,
                      uint32_t* scratch) {
   for (int j = 1; j < W; j++) {
@@ -71,6 +82,9 @@ void msm_build_table(hipStream_t st, uint32_t* table, uint64_t npts, int c, int 
     hipLaunchKernelGGL(k_batch_affine<32>, dim3(nb((npts + 31) / 32)), dim3(256), 0, st, cur, tmp_xyzz,
                        scratch, npts);
   }
+#ifndef KGS_ACC32
+  hipLaunchKernelGGL(k_tab_to29, dim3(nb(2 * (uint64_t)W * npts)), dim3(256), 0, st, table, 2 * (uint64_t)W * npts);
+#endif
 }
 
 // ------------------------------------------------------------------ digits + two-pass bucket sort
@@ -393,14 +407,15 @@ __device__ __forceinline__ void emit_run(uint32_t* bstart, uint32_t* segpart, ui
 }
 
 #ifndef KGS_ACC_WAVES
-#define KGS_ACC_WAVES 1
+#define KGS_ACC_WAVES 3
 #endif
 __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __restrict__ bstart, uint32_t* __restrict__ segpart,
                                                     uint32_t* __restrict__ segowner,
                                                     uint32_t* __restrict__ chunklist, uint32_t* __restrict__ chunkcnt,
                                                     const uint32_t* __restrict__ sorted,
                                                     const uint32_t* __restrict__ offsets, uint32_t nbins,
-                                                    const uint32_t* __restrict__ table, uint32_t L) {
+                                                    const uint32_t* __restrict__ table, uint32_t L,
+                                                    uint32_t* __restrict__ raw) {
   const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t E = offsets[nbins];
   const uint64_t start = s * L;
@@ -417,6 +432,7 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
   combine_enqueue(chunklist, chunkcnt, s, offsets[b], offsets[b + 1], L, 1);
   uint64_t rs = start;
   uint64_t bend = offsets[b + 1];
+#ifdef KGS_ACC32
   g1_xyzz acc = g1_xyzz::inf();
   for (uint64_t e = start; e < end; e++) {
     if (e >= bend) {
@@ -429,14 +445,51 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
     uint32_t v = sorted[e];
     g1_aff p = g1_aff::load(table + 16 * (uint64_t)(v & 0x7fffffffu));
     if (v & 0x80000000u) p.y = p.y.neg();
-#ifdef KGS_NO_LAZY
-    acc.add_aff(p);
-#else
     acc.add_aff_lazy(p);
-#endif
   }
   acc.canon();
   emit_run(bstart, segpart, b, rs, offsets, s, acc);
+#else
+  g1_acc29 acc;
+  acc.set_inf();
+  // software pipeline: the point of entry e+1 and the index of entry e+2 are in flight while
+  // entry e is added (the gathers' latency hides behind ~11 K cycles of VALU work)
+  uint32_t v = sorted[start];
+  uint32_t vn = start + 1 < end ? sorted[start + 1] : 0u;
+  const uint4* pt = reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(v & 0x7fffffffu));
+  uint4 a0 = pt[0], a1 = pt[1], a2 = pt[2], a3 = pt[3];
+  for (uint64_t e = start; e < end; e++) {
+    if (e >= bend) {
+      acc.store_raw(raw + RAW29_WORDS * (rs == offsets[b] ? (uint64_t)b : nbins + s));
+      do { b++; bend = offsets[b + 1]; } while (e >= bend);
+      rs = e;
+      acc.set_inf();
+    }
+    const uint32_t xw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const uint32_t yw[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+    const bool negy = (v & 0x80000000u) != 0;
+    if (e + 1 < end) {
+      const uint4* pn = reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(vn & 0x7fffffffu));
+      a0 = pn[0]; a1 = pn[1]; a2 = pn[2]; a3 = pn[3];
+      v = vn;
+      if (e + 2 < end) vn = sorted[e + 2];
+    }
+    acc.add_aff(xw, yw, negy);
+  }
+  acc.store_raw(raw + RAW29_WORDS * (rs == offsets[b] ? (uint64_t)b : nbins + s));
+#endif
+}
+
+// the accumulate kernel stores its runs in the fq29 form (a divergent per-lane conversion inside the
+// add loop would stall the whole wave); convert them all here: entry i < nbins -> bstart[i], else
+// segpart[i - nbins]. Entries that were never written are converted too and never read.
+__global__ void __launch_bounds__(256) k_raw29_convert(uint32_t* __restrict__ bstart, uint32_t* __restrict__ segpart,
+                                                       const uint32_t* __restrict__ raw, uint32_t nbins,
+                                                       uint64_t nseg) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nbins + nseg) return;
+  const g1_xyzz r = g1_acc29::load_raw(raw + RAW29_WORDS * i).to_xyzz();
+  r.store(i < nbins ? bstart + 32 * i : segpart + 32 * (i - nbins));
 }
 
 // Bucket totals. Bucket b = bstart[b] + the partials of the segments whose start lies strictly
@@ -601,16 +654,29 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
                      (const uint32_t*)w.digit, w.lo, hi_off, lob);
   if (ev) hipEventRecord(ev[1], st);
   const uint64_t E = N * (uint64_t)W;  // upper bound of nonzero entries
-  uint64_t L = E >> 18;
+  // one segment per resident thread (KGS_ACC_WAVES blocks of 256 per CU): every accumulate
+  // thread runs once and they all finish together (a second, partial round of blocks would
+  // leave most of the chip idle for a whole segment's duration)
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    return n;
+  }();
+  const uint64_t resident = (uint64_t)cus * KGS_ACC_WAVES * 256;
+  uint64_t L = (E + resident - 1) / resident;
   if (L < 4) L = 4;
-  if (L > 64) L = 64;
+  if ((E + L - 1) / L > (1ull << 18)) L = (E + (1ull << 18) - 1) >> 18;  // work buffers hold 2^18 + 2^16 segments
   const uint64_t nseg = (E + L - 1) / L;
   // chunk lists of the combine levels: list j holds <= nseg / CB_T^(j+1) + B entries
   uint32_t* cnt = w.chunkcnt;
   const uint64_t lcap = nseg / CB_T + B + 16;
   hipMemsetAsync(cnt, 0, 4 * CB_LEVELS, st);
   hipLaunchKernelGGL(k_accumulate, dim3(nb(nseg)), dim3(256), 0, st, w.bstart, w.segpart, w.segowner, w.chunklist,
-                     cnt, w.sorted, w.offsets, B + 1, tb.table, (uint32_t)L);
+                     cnt, w.sorted, w.offsets, B + 1, tb.table, (uint32_t)L, w.raw29);
+#ifndef KGS_ACC32
+  hipLaunchKernelGGL(k_raw29_convert, dim3(nb(B + 1 + nseg)), dim3(256), 0, st, w.bstart, w.segpart, w.raw29, B + 1,
+                     nseg);
+#endif
   if (ev) hipEventRecord(ev[2], st);
   uint64_t stride = 1, cap = lcap;
   for (int j = 0; j < CB_LEVELS; j++, stride *= CB_T) {

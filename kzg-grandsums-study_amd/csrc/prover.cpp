@@ -314,6 +314,7 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
     w.locnt = c.buf("msm_locnt" + sfx, 4 * 256 * 256 * 16);
     w.chunklist = c.buf("msm_chunklist" + sfx, 4 * 3 * (nseg / 16 + B + 16));
     w.chunkcnt = c.buf("msm_chunkcnt" + sfx, 64);
+    w.raw29 = c.buf("msm_raw29" + sfx, 160 * ((size_t)B + 2 + nseg));
     w.buckets = c.buf("msm_buckets" + sfx, 128 * (size_t)(B + 2));
     const uint32_t chunks = (B / 2 + 255) / 256 > 0 ? (B / 2 + 255) / 256 : 1;
     w.part = c.buf("msm_part" + sfx, 128 * (size_t)cc * chunks);

@@ -1,0 +1,169 @@
+"""CPU checks of the 9 x 29-bit Fq representation used by the MSM bucket accumulation
+(kzg-grandsums-study_amd/csrc/field29.hpp): its constants, and the interval analysis that proves
+no limb, column or value overflow in g1_acc29::add_aff for the exact multiples of q it uses.
+
+The GPU side is covered by the MSM / prover parity tests in test_gpu_parity.py (bit-exact
+commitments); this file pins the arithmetic argument those tests rely on.
+"""
+import math
+import os
+import re
+
+Q = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+MASK = (1 << 29) - 1
+RBITS = 261
+HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   "kzg-grandsums-study_amd", "csrc", "field29.hpp")
+
+
+def _hdr():
+    with open(HDR) as fh:
+        return fh.read()
+
+
+def _words(name, text):
+    m = re.search(r"%s\s*=\s*\{\{?([^}]*)\}" % re.escape(name), text)
+    assert m, name
+    return [int(x.strip().rstrip("u"), 16) for x in m.group(1).split(",") if x.strip()]
+
+
+def _d29(ws):
+    return sum(w << (29 * j) for j, w in enumerate(ws))
+
+
+def _d32(ws):
+    return sum(w << (32 * j) for j, w in enumerate(ws))
+
+
+def test_constants():
+    t = _hdr()
+    assert _d29(_words("L9 Q", t)) == Q
+    assert all(w <= MASK for w in _words("L9 Q", t))
+    assert _d29(_words("L9 ONE", t)) == pow(2, 261, Q)
+    assert _d29(_words("L9 C256", t)) == pow(2, 256, Q)
+    assert _d29(_words("L9 C266", t)) == pow(2, 266, Q)
+    assert _d32(_words("C261W[8]", t)) == pow(2, 261, Q)
+    inv = int(re.search(r"INV = (0x[0-9a-f]+)u", t).group(1), 16)
+    assert (Q * inv) % (1 << 29) == (1 << 29) - 1  # -q^-1 mod 2^29
+
+
+def _spread(k, s):
+    K = k * Q
+    d = [(K >> (29 * j)) & MASK for j in range(8)] + [K >> 232]
+    out = [d[0] + (s << 29)] + [d[j] + (s << 29) - s for j in range(1, 8)] + [d[8] - s]
+    assert sum(x << (29 * j) for j, x in enumerate(out)) == K
+    assert all(0 <= x < (1 << 32) for x in out)
+    return out
+
+
+class V:
+    """value < val, every limb <= limb (val may be refined per limb by the top limb bound)"""
+
+    def __init__(self, val, limb):
+        self.val, self.limb = val, limb
+
+    def limb_max(self, j):
+        return min(self.limb, (self.val - 1) >> (29 * j)) if j == 8 else self.limb
+
+
+def _mul(a, b):
+    col = 9 * a.limb * b.limb + 9 * MASK * MASK + (1 << 36)
+    assert col < (1 << 64), "column overflow %.3f" % math.log2(col)
+    out = (a.val * b.val >> RBITS) + Q + 1
+    assert out <= (1 << RBITS)
+    return V(out, MASK)
+
+
+def _add(a, b):
+    return V(a.val + b.val, a.limb + b.limb)
+
+
+def _sub(a, b, k, s):  # a + K - b, K = spread(k, s)
+    K = _spread(k, s)
+    for j in range(9):
+        assert K[j] >= b.limb_max(j), (k, s, j)
+    return V(a.val + k * Q, max(a.limb + K[j] for j in range(9)))
+
+
+def _neg(b, k, s):
+    return _sub(V(0, 0), b, k, s)
+
+
+def _norm(a):
+    assert a.val <= (1 << RBITS) and a.limb + 8 < (1 << 32)
+    return V(a.val, MASK)
+
+
+def madd_bound(vb):
+    """g1_acc29::add_aff step by step (same k, s as the header); returns the output bound"""
+    X1 = Y1 = ZZ1 = ZZZ1 = V(vb, MASK)
+    x2 = y2 = V(Q, MASK)
+    U2, S2 = _mul(x2, ZZ1), _mul(y2, ZZZ1)
+    P = _norm(_sub(U2, X1, 30, 1))
+    Rb = _neg(Y1, 32, 2)                      # K - Y1, then +- S2
+    for j in range(9):                        # the negated branch: K_j - Y1_j - S2_j >= 0
+        assert _spread(32, 2)[j] >= Y1.limb_max(j) + S2.limb_max(j)
+    R = _norm(V(Rb.val + S2.val, Rb.limb + S2.limb))
+    PP = _mul(P, P)
+    assert PP.val <= 8 * Q                    # maybe_zero8's candidate set covers PP
+    PPP, Qv, R2 = _mul(P, PP), _mul(X1, PP), _mul(R, R)
+    nX = _norm(_sub(R2, _add(PPP, _add(Qv, Qv)), 16, 3))
+    T = _sub(Qv, nX, 64, 1)
+    Y3 = _norm(_sub(_mul(R, T), _mul(Y1, PPP), 16, 1))
+    ZZ3, ZZZ3 = _mul(ZZ1, PP), _mul(ZZZ1, PPP)
+    # the raw-record conversion (to_fq) and the rare-path checks multiply by C256 < q
+    for c in (P, R, nX, Y3, ZZ3, ZZZ3):
+        assert _mul(c, V(Q, MASK)).val <= 2 * Q
+    return max(nX.val, Y3.val, ZZ3.val, ZZZ3.val)
+
+
+def test_add_aff_bounds_fixed_point():
+    # initial accumulator: a table point (< q) with ZZ = ZZZ = 2^261 mod q; negated y: 2q - y
+    vb = 2 * Q
+    for _ in range(50):
+        nxt = max(madd_bound(vb), vb)
+        if nxt == vb:
+            break
+        vb = nxt
+    assert madd_bound(vb) <= vb
+    assert math.log2(vb) < 258.6  # field29.hpp: coordinates < 2^258.6
+
+
+def test_spread_constants_used_by_header():
+    t = _hdr()
+    uses = set(re.findall(r"(?:sub|neg)<(\d+), (\d+)>", t))
+    assert uses == {("30", "1"), ("32", "2"), ("16", "3"), ("64", "1"), ("16", "1"), ("2", "1")}
+    for k, s in uses:
+        _spread(int(k), int(s))
+    # the initial negation 2q - y of a canonical y (< q) stays nonnegative per limb
+    K = _spread(2, 1)
+    assert all(K[j] >= (MASK if j < 8 else (Q - 1) >> 232) for j in range(9))
+
+
+def test_pack_unpack_roundtrip_model():
+    # python model of fq29::unpack / pack on random 256-bit values
+    import random
+    rnd = random.Random(7)
+    for _ in range(200):
+        x = rnd.getrandbits(255)
+        w = [(x >> (32 * i)) & 0xffffffff for i in range(8)]
+        limbs = []
+        for j in range(9):
+            bit = 29 * j
+            i, s = bit >> 5, bit & 31
+            v = w[i] >> s
+            if s > 3 and i + 1 < 8:
+                v |= (w[i + 1] << (32 - s)) & 0xffffffff
+            limbs.append(v & MASK)
+        assert _d29(limbs) == x
+        out = []
+        for i in range(8):
+            bit = 32 * i
+            j, s = bit // 29, bit % 29
+            v = limbs[j] >> s
+            if j + 1 < 9:
+                v |= (limbs[j + 1] << (29 - s)) & 0xffffffff
+            if s > 26 and j + 2 < 9:
+                v |= (limbs[j + 2] << (58 - s)) & 0xffffffff
+            out.append(v & 0xffffffff)
+        assert out == w
