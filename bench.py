@@ -64,9 +64,11 @@ def synth_evals(n, idx):
 
 BENCH_TAU = None
 # v_mad_u64_u32 issue rate of the whole chip: 256 CUs x 4 SIMDs x 64 lanes / 4.97 cycles x 2.4 GHz
-# (measured: profiles/ubench/issue_rates.hip); one 9 x 29-bit Montgomery product issues 162
+# (measured: profiles/ubench/issue_rates.hip). One bucket add (madd-2008-s in 9 x 29-bit limbs,
+# field29.hpp) issues 1,467 of them: 6 products x 162, 2 squares x 126 (45 symmetric partial
+# products + 81 for the reduction), and Y3 = R*T - Y1*PPP as one lazily reduced double product (243)
 MAD_PEAK = 256 * 4 * 64 / 4.97 * 2.4e9
-MADS_PER_PRODUCT = 162
+MADS_PER_ADD = 6 * 162 + 2 * 126 + 243
 
 
 def bench_tau():
@@ -377,14 +379,15 @@ def main():
     }
 
     # ---------------- roofline of the dominant kernel (k_accumulate)
-    # The kernel is integer-VALU issue bound. Algorithmic work per launch: entries x 1 mixed XYZZ add
-    # (madd-2008-s: 8M + 2S = 10 Fq Montgomery products) x 162 v_mad_u64_u32 per product (9 x 29-bit
-    # limbs, field29.hpp). Peak: the chip's measured v_mad_u64_u32 issue rate, MAD_PEAK (4.97 SIMD
-    # cycles per wave64 instruction at the 2.4 GHz nominal clock, profiles/ubench/ubench_r01.txt):
-    # frac = the share of the SIMDs' issue capacity spent on the product's multiply-adds.
+    # The kernel is integer-VALU issue bound. Work per launch: entries x 1 mixed XYZZ add (madd-2008-s:
+    # 8M + 2S = 10 Fq Montgomery products) = MADS_PER_ADD v_mad_u64_u32 (9 x 29-bit limbs,
+    # field29.hpp). Peak: the chip's measured v_mad_u64_u32 issue rate, MAD_PEAK (4.97 SIMD cycles
+    # per wave64 instruction at the 2.4 GHz nominal clock, profiles/ubench/ubench_r01.txt): frac = the
+    # share of the SIMDs' issue capacity spent on the products' multiply-adds. The accumulate phase is
+    # timed with HIP events on the MSM's stream around the k_accumulate launch alone.
     acc_ms = ph[1]
     mults = 10 * entries.value
-    achieved = mults * MADS_PER_PRODUCT / (acc_ms / 1e3) / 1e12
+    achieved = entries.value * MADS_PER_ADD / (acc_ms / 1e3) / 1e12
     peak = MAD_PEAK / 1e12
     traffic = None
     pmc_path = os.path.join(HERE, "profiles", "pmc_accumulate.json")

@@ -158,6 +158,77 @@ struct fq29 {
     return r;
   }
 
+#ifndef KGS_NO_SQR29
+  // Montgomery square a*a*2^-261: the CIOS rows of mul with the symmetric partial products taken
+  // once (2a_i * a_j, j > i, and a_i^2 on the diagonal): 45 + 81 mads instead of 162. Row i adds to
+  // absolute columns 2i..i+8, which sit at t[i..8] after i shifts. A column receives at most 5
+  // products (<= 2 * max(a_j)^2 each), so it stays below mul's bound for a normalised a.
+  __device__ __forceinline__ static fq29 sqr(const fq29& a) {
+    uint32_t d[9];
+#pragma unroll
+    for (int j = 0; j < 9; j++) d[j] = a.l[j] << 1;
+    uint64_t t[9];
+#pragma unroll
+    for (int j = 0; j < 9; j++) t[j] = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      t[i] = (uint64_t)a.l[i] * a.l[i] + t[i];
+#pragma unroll
+      for (int j = i + 1; j < 9; j++) t[j] = (uint64_t)d[i] * a.l[j] + t[j];
+      const uint32_t m = ((uint32_t)t[0] * f29::INV) & f29::MASK;
+      const uint64_t c = ((uint64_t)m * f29::Q.v[0] + t[0]) >> 29;
+#pragma unroll
+      for (int j = 1; j < 9; j++) t[j] = (uint64_t)m * f29::Q.v[j] + t[j];
+#pragma unroll
+      for (int j = 0; j < 8; j++) t[j] = t[j + 1];
+      t[0] += c;
+      t[8] = 0;
+    }
+    fq29 r;
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      const uint64_t s = t[j] + c;
+      r.l[j] = (uint32_t)s & f29::MASK;
+      c = s >> 29;
+    }
+    return r;
+  }
+  // (a*b + c*d)*2^-261 with ONE Montgomery reduction (lazy reduction of a sum of products): each CIOS
+  // row adds both rows of partial products before its reduction step, 243 mads instead of 324.
+  // Needs 9*(max a_j * max b_j + max c_j * max d_j) + 9*(2^29)^2 + 2^36 < 2^64 (all four normalised)
+  // and a*b + c*d < 2^261 * (2^261 - q); the result is normalised and < (a*b + c*d)/2^261 + q.
+  __device__ __forceinline__ static fq29 mul2(const fq29& a, const fq29& b, const fq29& c2, const fq29& d2) {
+    uint64_t t[9];
+#pragma unroll
+    for (int j = 0; j < 9; j++) t[j] = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+#pragma unroll
+      for (int j = 0; j < 9; j++) t[j] = (uint64_t)a.l[i] * b.l[j] + t[j];
+#pragma unroll
+      for (int j = 0; j < 9; j++) t[j] = (uint64_t)c2.l[i] * d2.l[j] + t[j];
+      const uint32_t m = ((uint32_t)t[0] * f29::INV) & f29::MASK;
+      const uint64_t c = ((uint64_t)m * f29::Q.v[0] + t[0]) >> 29;
+#pragma unroll
+      for (int j = 1; j < 9; j++) t[j] = (uint64_t)m * f29::Q.v[j] + t[j];
+#pragma unroll
+      for (int j = 0; j < 8; j++) t[j] = t[j + 1];
+      t[0] += c;
+      t[8] = 0;
+    }
+    fq29 r;
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      const uint64_t s = t[j] + c;
+      r.l[j] = (uint32_t)s & f29::MASK;
+      c = s >> 29;
+    }
+    return r;
+  }
+#endif
+
   // necessary condition for "== 0 mod q" of a normalised value < 8q: its low limb is (j*q) mod 2^29
   __device__ __forceinline__ bool maybe_zero8() const {
     bool z = false;
@@ -211,8 +282,12 @@ struct g1_acc29 {
 #pragma unroll
     for (int j = 0; j < 9; j++) R.l[j] = negy ? R.l[j] - S2.l[j] : R.l[j] + S2.l[j];
     R = R.norm();
-    const fq29 PP = fq29::mul(P, P);  // < 6.4 q
-    if (PP.maybe_zero8()) {           // rare: decide exactly
+#ifndef KGS_NO_SQR29
+    const fq29 PP = fq29::sqr(P);  // < 6.8 q
+#else
+    const fq29 PP = fq29::mul(P, P);
+#endif
+    if (PP.maybe_zero8()) {  // rare: decide exactly
       if (P.to_fq().is_zero()) {
         if (R.to_fq().is_zero()) {  // same point: doubling (256-bit path, converted back)
           g1_aff a;
@@ -230,6 +305,19 @@ struct g1_acc29 {
         return;
       }
     }
+#ifndef KGS_NO_SQR29
+    // ordered so that P, PP, ZZ, ZZZ and Qv die early: mul2 below has four operands live, and at
+    // <= 168 VGPRs the kernel keeps 3 waves per SIMD without spilling
+    const fq29 PPP = fq29::mul(P, PP);
+    ZZ = fq29::mul(ZZ, PP);
+    const fq29 Qv = fq29::mul(X, PP);
+    ZZZ = fq29::mul(ZZZ, PPP);
+    const fq29 R2 = fq29::sqr(R);
+    X = fq29::sub<16, 3>(R2, fq29::add(PPP, fq29::add(Qv, Qv))).norm();
+    const fq29 T = fq29::sub<64, 1>(Qv, X);
+    // Y3 = R*T - Y1*PPP = R*T + Y1*(3q - PPP) mod q, one reduction (PPP < 2.3q)
+    Y = fq29::mul2(R, T, Y, fq29::neg<3, 1>(PPP));
+#else
     const fq29 PPP = fq29::mul(P, PP);
     const fq29 Qv = fq29::mul(X, PP);
     const fq29 R2 = fq29::mul(R, R);
@@ -239,6 +327,7 @@ struct g1_acc29 {
     X = nX;
     ZZ = fq29::mul(ZZ, PP);
     ZZZ = fq29::mul(ZZZ, PPP);
+#endif
   }
 
   // raw form: 4 x 9 limbs + infinity flag, padded to 40 words (16-byte stores)

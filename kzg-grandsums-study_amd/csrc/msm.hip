@@ -452,31 +452,34 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
 #else
   g1_acc29 acc;
   acc.set_inf();
+  // entry indices fit 32 bits (offsets[] is uint32): fewer live VGPRs in the add loop
+  const uint32_t end32 = (uint32_t)end;
+  uint32_t rs32 = (uint32_t)start, bend32 = (uint32_t)bend;
   // software pipeline: the point of entry e+1 and the index of entry e+2 are in flight while
   // entry e is added (the gathers' latency hides behind ~11 K cycles of VALU work)
   uint32_t v = sorted[start];
   uint32_t vn = start + 1 < end ? sorted[start + 1] : 0u;
   const uint4* pt = reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(v & 0x7fffffffu));
   uint4 a0 = pt[0], a1 = pt[1], a2 = pt[2], a3 = pt[3];
-  for (uint64_t e = start; e < end; e++) {
-    if (e >= bend) {
-      acc.store_raw(raw + RAW29_WORDS * (rs == offsets[b] ? (uint64_t)b : nbins + s));
-      do { b++; bend = offsets[b + 1]; } while (e >= bend);
-      rs = e;
+  for (uint32_t e = (uint32_t)start; e < end32; e++) {
+    if (e >= bend32) {
+      acc.store_raw(raw + RAW29_WORDS * (rs32 == offsets[b] ? (uint64_t)b : nbins + s));
+      do { b++; bend32 = offsets[b + 1]; } while (e >= bend32);
+      rs32 = e;
       acc.set_inf();
     }
     const uint32_t xw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
     const uint32_t yw[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
     const bool negy = (v & 0x80000000u) != 0;
-    if (e + 1 < end) {
+    if (e + 1 < end32) {
       const uint4* pn = reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(vn & 0x7fffffffu));
       a0 = pn[0]; a1 = pn[1]; a2 = pn[2]; a3 = pn[3];
       v = vn;
-      if (e + 2 < end) vn = sorted[e + 2];
+      if (e + 2 < end32) vn = sorted[e + 2];
     }
     acc.add_aff(xw, yw, negy);
   }
-  acc.store_raw(raw + RAW29_WORDS * (rs == offsets[b] ? (uint64_t)b : nbins + s));
+  acc.store_raw(raw + RAW29_WORDS * (rs32 == offsets[b] ? (uint64_t)b : nbins + s));
 #endif
 }
 
@@ -618,8 +621,8 @@ __global__ void __launch_bounds__(64) k_bitsum2(uint32_t* __restrict__ T, const 
 // ------------------------------------------------------------------ driver (device part)
 void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* scalars, uint64_t N,
              uint32_t* T_out, hipEvent_t* ev) {
-  // ev (optional, 6 events): [0] start, [1] after digits+sort, [2] after accumulate,
-  // [3] after combine, [4] after bit-sum reduction
+  // ev (optional, 5 events): [0] start, [1] after digits+sort, [2] after k_accumulate,
+  // [3] after run conversion + combine, [4] after bit-sum reduction
   if (ev) hipEventRecord(ev[0], st);
   const int c = tb.c, W = tb.W;
   const uint32_t B = 1u << (c - 1);
@@ -673,11 +676,11 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   hipMemsetAsync(cnt, 0, 4 * CB_LEVELS, st);
   hipLaunchKernelGGL(k_accumulate, dim3(nb(nseg)), dim3(256), 0, st, w.bstart, w.segpart, w.segowner, w.chunklist,
                      cnt, w.sorted, w.offsets, B + 1, tb.table, (uint32_t)L, w.raw29);
+  if (ev) hipEventRecord(ev[2], st);  // the accumulate phase is the k_accumulate launch alone
 #ifndef KGS_ACC32
   hipLaunchKernelGGL(k_raw29_convert, dim3(nb(B + 1 + nseg)), dim3(256), 0, st, w.bstart, w.segpart, w.raw29, B + 1,
                      nseg);
 #endif
-  if (ev) hipEventRecord(ev[2], st);
   uint64_t stride = 1, cap = lcap;
   for (int j = 0; j < CB_LEVELS; j++, stride *= CB_T) {
     uint32_t* lin = w.chunklist + (uint64_t)j * lcap;

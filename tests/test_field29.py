@@ -9,6 +9,8 @@ import math
 import os
 import re
 
+import pytest
+
 Q = 21888242871839275222246405745257275088696311157297823662689037894645226208583
 MASK = (1 << 29) - 1
 RBITS = 261
@@ -74,6 +76,24 @@ def _mul(a, b):
     return V(out, MASK)
 
 
+def _sqr(a):  # fq29::sqr: <= 5 products per column, each <= 2 * limb^2
+    col = 10 * a.limb * a.limb + 9 * MASK * MASK + (1 << 36)
+    assert col < (1 << 64), "column overflow %.3f" % math.log2(col)
+    out = (a.val * a.val >> RBITS) + Q + 1
+    assert out <= (1 << RBITS)
+    return V(out, MASK)
+
+
+def _mul2(a, b, c, d):  # fq29::mul2: (a*b + c*d) / 2^261, one reduction
+    col = 9 * (a.limb * b.limb + c.limb * d.limb) + 9 * MASK * MASK + (1 << 36)
+    assert col < (1 << 64), "column overflow %.3f" % math.log2(col)
+    s = a.val * b.val + c.val * d.val
+    assert s < (1 << RBITS) * ((1 << RBITS) - Q)
+    out = (s >> RBITS) + Q + 1
+    assert out <= (1 << RBITS)
+    return V(out, MASK)
+
+
 def _add(a, b):
     return V(a.val + b.val, a.limb + b.limb)
 
@@ -94,8 +114,10 @@ def _norm(a):
     return V(a.val, MASK)
 
 
-def madd_bound(vb):
-    """g1_acc29::add_aff step by step (same k, s as the header); returns the output bound"""
+def madd_bound(vb, legacy=False):
+    """g1_acc29::add_aff step by step (same k, s as the header); returns the output bound.
+    legacy=True models the -DKGS_NO_SQR29 build (plain products, Y3 from two reduced products)."""
+    sqr = (lambda a: _mul(a, a)) if legacy else _sqr
     X1 = Y1 = ZZ1 = ZZZ1 = V(vb, MASK)
     x2 = y2 = V(Q, MASK)
     U2, S2 = _mul(x2, ZZ1), _mul(y2, ZZZ1)
@@ -104,12 +126,15 @@ def madd_bound(vb):
     for j in range(9):                        # the negated branch: K_j - Y1_j - S2_j >= 0
         assert _spread(32, 2)[j] >= Y1.limb_max(j) + S2.limb_max(j)
     R = _norm(V(Rb.val + S2.val, Rb.limb + S2.limb))
-    PP = _mul(P, P)
+    PP = sqr(P)
     assert PP.val <= 8 * Q                    # maybe_zero8's candidate set covers PP
-    PPP, Qv, R2 = _mul(P, PP), _mul(X1, PP), _mul(R, R)
+    PPP, Qv, R2 = _mul(P, PP), _mul(X1, PP), sqr(R)
     nX = _norm(_sub(R2, _add(PPP, _add(Qv, Qv)), 16, 3))
     T = _sub(Qv, nX, 64, 1)
-    Y3 = _norm(_sub(_mul(R, T), _mul(Y1, PPP), 16, 1))
+    if legacy:
+        Y3 = _norm(_sub(_mul(R, T), _mul(Y1, PPP), 16, 1))
+    else:
+        Y3 = _mul2(R, T, Y1, _neg(PPP, 3, 1))  # R*T + Y1*(3q - PPP)
     ZZ3, ZZZ3 = _mul(ZZ1, PP), _mul(ZZZ1, PPP)
     # the raw-record conversion (to_fq) and the rare-path checks multiply by C256 < q
     for c in (P, R, nX, Y3, ZZ3, ZZZ3):
@@ -117,22 +142,23 @@ def madd_bound(vb):
     return max(nX.val, Y3.val, ZZ3.val, ZZZ3.val)
 
 
-def test_add_aff_bounds_fixed_point():
+@pytest.mark.parametrize("legacy", [False, True])
+def test_add_aff_bounds_fixed_point(legacy):
     # initial accumulator: a table point (< q) with ZZ = ZZZ = 2^261 mod q; negated y: 2q - y
     vb = 2 * Q
     for _ in range(50):
-        nxt = max(madd_bound(vb), vb)
+        nxt = max(madd_bound(vb, legacy), vb)
         if nxt == vb:
             break
         vb = nxt
-    assert madd_bound(vb) <= vb
+    assert madd_bound(vb, legacy) <= vb
     assert math.log2(vb) < 258.6  # field29.hpp: coordinates < 2^258.6
 
 
 def test_spread_constants_used_by_header():
     t = _hdr()
     uses = set(re.findall(r"(?:sub|neg)<(\d+), (\d+)>", t))
-    assert uses == {("30", "1"), ("32", "2"), ("16", "3"), ("64", "1"), ("16", "1"), ("2", "1")}
+    assert uses == {("30", "1"), ("32", "2"), ("16", "3"), ("64", "1"), ("16", "1"), ("2", "1"), ("3", "1")}
     for k, s in uses:
         _spread(int(k), int(s))
     # the initial negation 2q - y of a canonical y (< q) stays nonnegative per limb
@@ -167,3 +193,54 @@ def test_pack_unpack_roundtrip_model():
                 v |= (limbs[j + 2] << (58 - s)) & 0xffffffff
             out.append(v & 0xffffffff)
         assert out == w
+
+
+def _cios(rows):
+    """fq29 CIOS loop of mul/sqr/mul2 on Python ints: rows(i) -> list of (absolute column offset j,
+    product) pairs added in row i; every 64-bit column accumulator is checked for overflow."""
+    qv = [(Q >> (29 * j)) & MASK for j in range(8)] + [Q >> 232]
+    inv = (-pow(Q, -1, 1 << 29)) % (1 << 29)
+    t = [0] * 9
+    for i in range(9):
+        for j, p in rows(i):
+            t[j] += p
+            assert t[j] < (1 << 64)
+        m = (t[0] * inv) & MASK
+        c = (m * qv[0] + t[0]) >> 29
+        for j in range(1, 9):
+            t[j] += m * qv[j]
+            assert t[j] < (1 << 64)
+        t = t[1:] + [0]
+        t[0] += c
+    r, c = [], 0
+    for j in range(9):
+        s = t[j] + c
+        r.append(s & MASK)
+        c = s >> 29
+    r[8] += c << 29
+    return _d29(r)
+
+
+def _limbs(x):
+    return [(x >> (29 * j)) & MASK for j in range(8)] + [x >> 232]
+
+
+def test_sqr_mul2_model():
+    # the exact row schedules of fq29::sqr and fq29::mul2 on random inputs at their bound limits
+    import random
+    rnd = random.Random(11)
+    rinv = pow(2, -261, Q)
+    for _ in range(300):
+        a = rnd.randrange(1 << 258)
+        al = _limbs(a)
+        d = [2 * x for x in al]
+        sq = _cios(lambda i: [(i, al[i] * al[i])] + [(j, d[i] * al[j]) for j in range(i + 1, 9)])
+        assert sq % Q == a * a * rinv % Q and sq < (a * a >> 261) + Q + 1
+        # mul2 with unnormalised second factors (limbs up to 2^30.6 / 2^29.8 as in add_aff)
+        b, c, e = rnd.randrange(1 << 258), rnd.randrange(1 << 258), rnd.randrange(1 << 255)
+        bl, cl, el = _limbs(b), _limbs(c), _limbs(e)
+        bl = [x + (1 << 30) if j < 8 else x for j, x in enumerate(bl)]  # same value + spread carries
+        bl = [bl[0]] + [bl[j] - 2 if j < 8 else bl[j] - 2 for j in range(1, 9)]
+        bval = _d29(bl)
+        m2 = _cios(lambda i: [(j, al[i] * bl[j]) for j in range(9)] + [(j, cl[i] * el[j]) for j in range(9)])
+        assert m2 % Q == (a * bval + c * e) * rinv % Q
