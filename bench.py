@@ -379,16 +379,19 @@ def main():
     }
 
     # ---------------- roofline of the dominant kernel (k_accumulate)
-    # The kernel is integer-VALU issue bound. Work per launch: entries x 1 mixed XYZZ add (madd-2008-s:
-    # 8M + 2S = 10 Fq Montgomery products) = MADS_PER_ADD v_mad_u64_u32 (9 x 29-bit limbs,
-    # field29.hpp). Peak: the chip's measured v_mad_u64_u32 issue rate, MAD_PEAK (4.97 SIMD cycles
-    # per wave64 instruction at the 2.4 GHz nominal clock, profiles/ubench/ubench_r01.txt): frac = the
-    # share of the SIMDs' issue capacity spent on the products' multiply-adds. The accumulate phase is
-    # timed with HIP events on the MSM's stream around the k_accumulate launch alone.
+    # The kernel is integer-VALU issue bound. Algorithmic work per launch: entries x 1 mixed XYZZ add
+    # (madd-2008-s: 8M + 2S = 10 Fq Montgomery products). Peak: the Fq-product rate at which the
+    # chip's measured v_mad_u64_u32 issue rate (MAD_PEAK: 4.97 SIMD cycles per wave64 instruction at
+    # the 2.4 GHz nominal clock, profiles/ubench/ubench_r01.txt) is spent on nothing but the 162 mads
+    # of a 9 x 29-bit Montgomery product (field29.hpp) — no carries, loads or control. The kernel's own
+    # instruction stream is leaner per add (MADS_PER_ADD: squares and the lazily reduced Y3 save 153
+    # mads) and carries ~40 % non-mad instructions, so frac measures how close the whole add gets to
+    # that mad-only product rate. Timed with HIP events on the MSM's stream around the k_accumulate
+    # launch alone.
     acc_ms = ph[1]
     mults = 10 * entries.value
-    achieved = entries.value * MADS_PER_ADD / (acc_ms / 1e3) / 1e12
-    peak = MAD_PEAK / 1e12
+    achieved = mults / (acc_ms / 1e3) / 1e9
+    peak = MAD_PEAK / 162 / 1e9
     traffic = None
     pmc_path = os.path.join(HERE, "profiles", "pmc_accumulate.json")
     if os.path.exists(pmc_path):
@@ -397,9 +400,10 @@ def main():
                 traffic = json.load(fh).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    roofline = {"bound": "valu", "kernel": "k_accumulate", "achieved": round(achieved, 3), "peak": round(peak, 3),
-                "unit": "T v_mad_u64_u32/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                "fq_products_per_s": round(mults / (acc_ms / 1e3)), "g1_adds_per_s": round(entries.value / (acc_ms / 1e3)),
+    roofline = {"bound": "valu", "kernel": "k_accumulate", "achieved": round(achieved, 2), "peak": round(peak, 2),
+                "unit": "G Fq-products/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                "mad_issue_frac": round(entries.value * MADS_PER_ADD / (acc_ms / 1e3) / MAD_PEAK, 4),
+                "g1_adds_per_s": round(entries.value / (acc_ms / 1e3)),
                 "algorithmic_bytes_per_launch": 68 * entries.value,
                 "hbm_gbps_algorithmic": round(68 * entries.value / (acc_ms / 1e3) / 1e9, 1)}
 

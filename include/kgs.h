@@ -160,7 +160,7 @@ int kgs_keccak256(const uint8_t* data, uint64_t len, uint8_t out[32]);
 int kgs_bench_msm(kgs_ctx_t* ctx, const void* d_scalars_mont, uint64_t n, int reps, double* ms);
 /* Run `reps` MSMs of n scalars, accumulating per-phase device time (ms) into phase_ms[4]:
  * [0] digit recoding + counting sort, [1] bucket accumulation (the k_accumulate launch alone),
- * [2] run conversion + bucket combine, [3] bit-sum reduction. *entries = nonzero (bucket, point) entries of the last run. */
+ * [2] bucket combine, [3] bit-sum reduction. *entries = nonzero (bucket, point) entries of the last run. */
 int kgs_bench_msm_phases(kgs_ctx_t* ctx, const void* d_scalars_mont, uint64_t n, int reps, double* phase_ms,
                          uint64_t* entries);
 /* Run `reps` forward+inverse NTT pairs of size 2^logm on a device buffer; returns ms. */

@@ -158,7 +158,6 @@ struct fq29 {
     return r;
   }
 
-#ifndef KGS_NO_SQR29
   // Montgomery square a*a*2^-261: the CIOS rows of mul with the symmetric partial products taken
   // once (2a_i * a_j, j > i, and a_i^2 on the diagonal): 45 + 81 mads instead of 162. Row i adds to
   // absolute columns 2i..i+8, which sit at t[i..8] after i shifts. A column receives at most 5
@@ -227,7 +226,6 @@ struct fq29 {
     }
     return r;
   }
-#endif
 
   // necessary condition for "== 0 mod q" of a normalised value < 8q: its low limb is (j*q) mod 2^29
   __device__ __forceinline__ bool maybe_zero8() const {
@@ -328,6 +326,56 @@ struct g1_acc29 {
     ZZ = fq29::mul(ZZ, PP);
     ZZZ = fq29::mul(ZZZ, PPP);
 #endif
+  }
+
+  // this += o, both accumulators (add-2008-s; coordinates < 2^258.6, normalised): the bucket
+  // combine and bit-sum trees. 10 products + 2 squares + the lazily reduced Y3. The CIOS rows give
+  // 9 independent column chains, so a lone wave (these trees run at low occupancy) is far less
+  // latency-bound than with the 8 x 32-bit product-scanning chain. Special cases as g1_xyzz::add;
+  // the doubling (equal points, never met by distinct buckets in practice) goes through the 256-bit
+  // path and is converted back.
+  __device__ __forceinline__ void add(const g1_acc29& o) {
+    if (o.inf) return;
+    if (inf) {
+      *this = o;
+      return;
+    }
+    const fq29 U1 = fq29::mul(X, o.ZZ);
+    const fq29 U2 = fq29::mul(o.X, ZZ);
+    const fq29 S1 = fq29::mul(Y, o.ZZZ);
+    const fq29 S2 = fq29::mul(o.Y, ZZZ);
+    const fq29 P = fq29::sub<8, 1>(U2, U1).norm();
+    const fq29 R = fq29::sub<8, 1>(S2, S1).norm();
+    const fq29 PP = fq29::sqr(P);
+    if (PP.maybe_zero8()) {
+      if (P.to_fq().is_zero()) {
+        if (R.to_fq().is_zero()) {
+          *this = from_xyzz(to_xyzz().dbl());
+        } else {
+          inf = true;
+        }
+        return;
+      }
+    }
+    const fq29 PPP = fq29::mul(P, PP);
+    ZZ = fq29::mul(fq29::mul(ZZ, o.ZZ), PP);
+    ZZZ = fq29::mul(fq29::mul(ZZZ, o.ZZZ), PPP);
+    const fq29 Qv = fq29::mul(U1, PP);
+    const fq29 R2 = fq29::sqr(R);
+    X = fq29::sub<16, 3>(R2, fq29::add(PPP, fq29::add(Qv, Qv))).norm();
+    const fq29 T = fq29::sub<64, 1>(Qv, X);
+    Y = fq29::mul2(R, T, S1, fq29::neg<3, 1>(PPP));  // R*T - S1*PPP
+  }
+
+  // canonical 256-bit-Montgomery XYZZ -> accumulator (coordinates < 2q, normalised)
+  __device__ __forceinline__ static g1_acc29 from_xyzz(const g1_xyzz& p) {
+    g1_acc29 a;
+    a.inf = p.is_inf();
+    a.X = fq29::from_fq(p.X);
+    a.Y = fq29::from_fq(p.Y);
+    a.ZZ = fq29::from_fq(p.ZZ);
+    a.ZZZ = fq29::from_fq(p.ZZZ);
+    return a;
   }
 
   // raw form: 4 x 9 limbs + infinity flag, padded to 40 words (16-byte stores)

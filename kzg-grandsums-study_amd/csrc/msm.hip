@@ -82,9 +82,7 @@ void msm_build_table(hipStream_t st, uint32_t* table, uint64_t npts, int c, int 
     hipLaunchKernelGGL(k_batch_affine<32>, dim3(nb((npts + 31) / 32)), dim3(256), 0, st, cur, tmp_xyzz,
                        scratch, npts);
   }
-#ifndef KGS_ACC32
   hipLaunchKernelGGL(k_tab_to29, dim3(nb(2 * (uint64_t)W * npts)), dim3(256), 0, st, table, 2 * (uint64_t)W * npts);
-#endif
 }
 
 // ------------------------------------------------------------------ digits + two-pass bucket sort
@@ -391,26 +389,23 @@ constexpr int CB_LEVELS = 3;
 // when its bucket has more than CB_T partials and s is aligned: append it to that level's list.
 __device__ __forceinline__ void combine_enqueue(uint32_t* list, uint32_t* cnt, uint64_t s, uint64_t o0, uint64_t o1,
                                                 uint32_t L, uint64_t stride) {
-  if (s * L <= o0) return;  // the segment's first run starts its bucket (bstart), not a partial
+  if (s * L <= o0) return;  // the segment's first run starts its bucket (run_rec b), not a partial
   const uint64_t s_lo = o0 / L + 1, s_hi = (o1 + L - 1) / L;
   if (s_hi - s_lo <= CB_T) return;  // short list: summed directly by k_combine
   if ((s - s_lo) % (stride * CB_T) != 0 || s + stride >= s_hi) return;
   list[atomicAdd(cnt, 1u)] = (uint32_t)s;
 }
 
-__device__ __forceinline__ void emit_run(uint32_t* bstart, uint32_t* segpart, uint32_t b, uint64_t rs,
-                                         const uint32_t* offsets, uint64_t seg, const g1_xyzz& acc) {
-  if (rs == offsets[b])
-    acc.store(bstart + 32 * (uint64_t)b);
-  else
-    acc.store(segpart + 32 * seg);
-}
+// Run records (g1_acc29 raw form, RAW29_WORDS words each) of one MSM live in ONE array `raw`:
+// record b < nbins = B + 1 is the run that starts bucket b (later overwritten by the bucket's
+// total), record nbins + s the partial of segment s (a run that started before the segment).
+__device__ __forceinline__ uint32_t* run_rec(uint32_t* raw, uint64_t i) { return raw + RAW29_WORDS * i; }
+__device__ __forceinline__ const uint32_t* run_rec(const uint32_t* raw, uint64_t i) { return raw + RAW29_WORDS * i; }
 
 #ifndef KGS_ACC_WAVES
 #define KGS_ACC_WAVES 3
 #endif
-__global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __restrict__ bstart, uint32_t* __restrict__ segpart,
-                                                    uint32_t* __restrict__ segowner,
+__global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __restrict__ segowner,
                                                     uint32_t* __restrict__ chunklist, uint32_t* __restrict__ chunkcnt,
                                                     const uint32_t* __restrict__ sorted,
                                                     const uint32_t* __restrict__ offsets, uint32_t nbins,
@@ -430,31 +425,11 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
   uint32_t b = lo;
   segowner[s] = b;  // bucket of the segment's first run (read by the combine levels)
   combine_enqueue(chunklist, chunkcnt, s, offsets[b], offsets[b + 1], L, 1);
-  uint64_t rs = start;
-  uint64_t bend = offsets[b + 1];
-#ifdef KGS_ACC32
-  g1_xyzz acc = g1_xyzz::inf();
-  for (uint64_t e = start; e < end; e++) {
-    if (e >= bend) {
-      acc.canon();
-      emit_run(bstart, segpart, b, rs, offsets, s, acc);
-      do { b++; bend = offsets[b + 1]; } while (e >= bend);
-      rs = e;
-      acc = g1_xyzz::inf();
-    }
-    uint32_t v = sorted[e];
-    g1_aff p = g1_aff::load(table + 16 * (uint64_t)(v & 0x7fffffffu));
-    if (v & 0x80000000u) p.y = p.y.neg();
-    acc.add_aff_lazy(p);
-  }
-  acc.canon();
-  emit_run(bstart, segpart, b, rs, offsets, s, acc);
-#else
   g1_acc29 acc;
   acc.set_inf();
   // entry indices fit 32 bits (offsets[] is uint32): fewer live VGPRs in the add loop
   const uint32_t end32 = (uint32_t)end;
-  uint32_t rs32 = (uint32_t)start, bend32 = (uint32_t)bend;
+  uint32_t rs32 = (uint32_t)start, bend32 = offsets[b + 1];
   // software pipeline: the point of entry e+1 and the index of entry e+2 are in flight while
   // entry e is added (the gathers' latency hides behind ~11 K cycles of VALU work)
   uint32_t v = sorted[start];
@@ -463,7 +438,7 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
   uint4 a0 = pt[0], a1 = pt[1], a2 = pt[2], a3 = pt[3];
   for (uint32_t e = (uint32_t)start; e < end32; e++) {
     if (e >= bend32) {
-      acc.store_raw(raw + RAW29_WORDS * (rs32 == offsets[b] ? (uint64_t)b : nbins + s));
+      acc.store_raw(run_rec(raw, rs32 == offsets[b] ? (uint64_t)b : nbins + s));
       do { b++; bend32 = offsets[b + 1]; } while (e >= bend32);
       rs32 = e;
       acc.set_inf();
@@ -479,45 +454,35 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
     }
     acc.add_aff(xw, yw, negy);
   }
-  acc.store_raw(raw + RAW29_WORDS * (rs32 == offsets[b] ? (uint64_t)b : nbins + s));
-#endif
+  acc.store_raw(run_rec(raw, rs32 == offsets[b] ? (uint64_t)b : nbins + s));
 }
 
-// the accumulate kernel stores its runs in the fq29 form (a divergent per-lane conversion inside the
-// add loop would stall the whole wave); convert them all here: entry i < nbins -> bstart[i], else
-// segpart[i - nbins]. Entries that were never written are converted too and never read.
-__global__ void __launch_bounds__(256) k_raw29_convert(uint32_t* __restrict__ bstart, uint32_t* __restrict__ segpart,
-                                                       const uint32_t* __restrict__ raw, uint32_t nbins,
-                                                       uint64_t nseg) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nbins + nseg) return;
-  const g1_xyzz r = g1_acc29::load_raw(raw + RAW29_WORDS * i).to_xyzz();
-  r.store(i < nbins ? bstart + 32 * i : segpart + 32 * (i - nbins));
-}
-
-// Bucket totals. Bucket b = bstart[b] + the partials of the segments whose start lies strictly
-// inside it: segments s_lo(b) = offsets[b]/L + 1 .. s_hi(b) = ceil(offsets[b+1]/L) - 1. Buckets can be
-// arbitrarily skewed (a selector polynomial has all-equal coefficients, so every point lands in the
-// same bucket of each window), so the partials are first reduced in CB_LEVELS chunked levels: at
-// level j the thread of segment s = s_lo + i*CB_T^(j+1) adds the CB_T partials at stride CB_T^j that
-// follow it (in place). The final pass then has <= ceil(m / CB_T^CB_LEVELS) partials per bucket, two
-// lanes per bucket joined by one xor-shuffle add. Depth for m partials: ~CB_T*CB_LEVELS + m/CB_T^3.
-// Lists of <= CB_T partials (every bucket of a uniform scalar distribution) skip the levels.
-__device__ __forceinline__ g1_xyzz shfl_xor_pt(const g1_xyzz& a, int mask) {
-  g1_xyzz r;
+// Bucket totals. Bucket b = its start record (run_rec b) + the partials of the segments whose start
+// lies strictly inside it: segments s_lo(b) = offsets[b]/L + 1 .. s_hi(b) = ceil(offsets[b+1]/L) - 1.
+// Buckets can be arbitrarily skewed (a selector polynomial has all-equal coefficients, so every point
+// lands in the same bucket of each window), so the partials are first reduced in CB_LEVELS chunked
+// levels: at level j the thread of segment s = s_lo + i*CB_T^(j+1) adds the CB_T partials at stride
+// CB_T^j that follow it (in place). The final pass then has <= ceil(m / CB_T^CB_LEVELS) partials per
+// bucket, two lanes per bucket joined by one xor-shuffle add. Depth for m partials:
+// ~CB_T*CB_LEVELS + m/CB_T^3. Lists of <= CB_T partials (every bucket of a uniform scalar
+// distribution) skip the levels. All of the tail (combine, bit sums) adds run records in the fq29
+// form with g1_acc29::add; only the c bit sums leave as 256-bit XYZZ points for the host.
+__device__ __forceinline__ g1_acc29 shfl_xor_acc(const g1_acc29& a, int mask) {
+  g1_acc29 r;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    r.X.v[i] = __shfl_xor(a.X.v[i], mask);
-    r.Y.v[i] = __shfl_xor(a.Y.v[i], mask);
-    r.ZZ.v[i] = __shfl_xor(a.ZZ.v[i], mask);
-    r.ZZZ.v[i] = __shfl_xor(a.ZZZ.v[i], mask);
+  for (int j = 0; j < 9; j++) {
+    r.X.l[j] = __shfl_xor(a.X.l[j], mask);
+    r.Y.l[j] = __shfl_xor(a.Y.l[j], mask);
+    r.ZZ.l[j] = __shfl_xor(a.ZZ.l[j], mask);
+    r.ZZZ.l[j] = __shfl_xor(a.ZZZ.l[j], mask);
   }
+  r.inf = __shfl_xor((int)a.inf, mask) != 0;
   return r;
 }
 
 // level j: one thread per listed chunk start s (stride CB_T^j): add the CB_T - 1 partials that follow
 // at that stride, store in place, and list s for level j + 1 if it starts a chunk there
-__global__ void __launch_bounds__(256) k_combine_level(uint32_t* __restrict__ segpart,
+__global__ void __launch_bounds__(256) k_combine_level(uint32_t* __restrict__ raw, uint32_t nbins,
                                                        const uint32_t* __restrict__ segowner,
                                                        const uint32_t* __restrict__ offsets,
                                                        const uint32_t* __restrict__ list_in,
@@ -531,31 +496,33 @@ __global__ void __launch_bounds__(256) k_combine_level(uint32_t* __restrict__ se
   const uint64_t o0 = offsets[b], o1 = offsets[b + 1];
   const uint64_t s_hi = (o1 + L - 1) / L;
   const uint64_t top = s + stride * CB_T < s_hi ? s + stride * CB_T : s_hi;
-  g1_xyzz acc = g1_xyzz::load(segpart + 32 * s);
-  for (uint64_t u = s + stride; u < top; u += stride) acc.add(g1_xyzz::load(segpart + 32 * u));
-  acc.store(segpart + 32 * s);
+  g1_acc29 acc = g1_acc29::load_raw(run_rec(raw, nbins + s));
+  for (uint64_t u = s + stride; u < top; u += stride) acc.add(g1_acc29::load_raw(run_rec(raw, nbins + u)));
+  acc.store_raw(run_rec(raw, nbins + s));
   if (list_out) combine_enqueue(list_out, cnt_out, s, o0, o1, L, stride * CB_T);
 }
 
-__global__ void __launch_bounds__(256) k_combine(uint32_t* __restrict__ buckets, const uint32_t* __restrict__ bstart,
-                                                 const uint32_t* __restrict__ segpart,
+// bucket b's total replaces its start record (run_rec b), for every b in 1..B (empty: infinity)
+__global__ void __launch_bounds__(256) k_combine(uint32_t* __restrict__ raw, uint32_t nbins,
                                                  const uint32_t* __restrict__ offsets, uint32_t B, uint32_t L,
                                                  uint64_t stride) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t b = (g >> 1) + 1;  // buckets 1..B
   const uint32_t sub = g & 1;
-  g1_xyzz acc = g1_xyzz::inf();
+  g1_acc29 acc;
+  acc.set_inf();
   if (b <= B) {
     const uint64_t o0 = offsets[b], o1 = offsets[b + 1];
     if (o1 > o0) {
-      if (sub == 0) acc = g1_xyzz::load(bstart + 32 * (uint64_t)b);
+      if (sub == 0) acc = g1_acc29::load_raw(run_rec(raw, b));
       const uint64_t s_lo = o0 / L + 1, s_hi = (o1 + L - 1) / L;
       const uint64_t st = s_hi > s_lo + CB_T ? stride : 1;  // reduced by the levels, or short
-      for (uint64_t sgm = s_lo + sub * st; sgm < s_hi; sgm += 2 * st) acc.add(g1_xyzz::load(segpart + 32 * sgm));
+      for (uint64_t sgm = s_lo + sub * st; sgm < s_hi; sgm += 2 * st)
+        acc.add(g1_acc29::load_raw(run_rec(raw, nbins + sgm)));
     }
   }
-  acc.add(shfl_xor_pt(acc, 1));
-  if (b <= B && sub == 0) acc.store(buckets + 32 * (uint64_t)b);
+  acc.add(shfl_xor_acc(acc, 1));
+  if (b <= B && sub == 0) acc.store_raw(run_rec(raw, b));
 }
 
 // ------------------------------------------------------------------ sum_b b*S_b via bit sums
@@ -569,60 +536,65 @@ __global__ void __launch_bounds__(256) k_combine(uint32_t* __restrict__ buckets,
 constexpr int BS_CHAIN = KGS_BS_CHAIN;
 constexpr uint32_t BS_SPAN = 256 * BS_CHAIN;  // buckets per block
 
-__device__ __forceinline__ g1_xyzz block_tree_sum256(g1_xyzz v, uint32_t* lds) {
+__device__ __forceinline__ g1_acc29 block_tree_sum256(g1_acc29 v, uint32_t* lds) {
   for (int stride = 128; stride > 0; stride >>= 1) {
-    if (threadIdx.x >= stride && threadIdx.x < 2 * stride) v.store(lds + 32 * (threadIdx.x - stride));
+    if (threadIdx.x >= stride && threadIdx.x < 2 * stride) v.store_raw(lds + RAW29_WORDS * (threadIdx.x - stride));
     __syncthreads();
-    if (threadIdx.x < stride) v.add(g1_xyzz::load(lds + 32 * threadIdx.x));
+    if (threadIdx.x < stride) v.add(g1_acc29::load_raw(lds + RAW29_WORDS * threadIdx.x));
     __syncthreads();
   }
   return v;
 }
 
-__global__ void __launch_bounds__(256) k_bitsum1(uint32_t* __restrict__ part, const uint32_t* __restrict__ buckets,
+// part: c x chunks run records; the bucket totals are run_rec(raw, b)
+__global__ void __launch_bounds__(256) k_bitsum1(uint32_t* __restrict__ part, const uint32_t* __restrict__ raw,
                                                  int c, uint32_t chunks) {
-  __shared__ uint32_t lds[128 * 32];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[128 * RAW29_WORDS];
   const int k = blockIdx.y;
   const uint32_t chunk = blockIdx.x;
   const uint32_t B = 1u << (c - 1);
-  g1_xyzz v = g1_xyzz::inf();
+  g1_acc29 v;
+  v.set_inf();
   if (k == c - 1) {
-    if (chunk == 0 && threadIdx.x == 0) v = g1_xyzz::load(buckets + 32 * (uint64_t)B);
+    if (chunk == 0 && threadIdx.x == 0) v = g1_acc29::load_raw(run_rec(raw, B));
   } else {
 #pragma unroll 1
     for (int i = 0; i < BS_CHAIN; i++) {
       const uint32_t t = chunk * BS_SPAN + i * 256 + threadIdx.x;
       if (t < B / 2) {
         const uint32_t b = ((t >> k) << (k + 1)) | (1u << k) | (t & ((1u << k) - 1));
-        v.add(g1_xyzz::load(buckets + 32 * (uint64_t)b));
+        v.add(g1_acc29::load_raw(run_rec(raw, b)));
       }
     }
   }
+  uint32_t* out = part + (uint64_t)RAW29_WORDS * ((uint64_t)k * chunks + chunk);
   if (k == c - 1 && chunk > 0) {  // uniform per block: an empty partial
-    if (threadIdx.x == 0) v.store(part + 32 * ((uint64_t)k * chunks + chunk));
+    if (threadIdx.x == 0) v.store_raw(out);
     return;
   }
   v = block_tree_sum256(v, lds);
-  if (threadIdx.x == 0) v.store(part + 32 * ((uint64_t)k * chunks + chunk));
+  if (threadIdx.x == 0) v.store_raw(out);
 }
 
-// one wave per k: sum the chunk partials (<= 64 per lane pass), xor-shuffle tree
+// one wave per k: sum the chunk partials (<= 64 per lane pass), xor-shuffle tree, 256-bit XYZZ out
 __global__ void __launch_bounds__(64) k_bitsum2(uint32_t* __restrict__ T, const uint32_t* __restrict__ part,
                                                 uint32_t chunks) {
   const int k = blockIdx.x;
-  g1_xyzz v = g1_xyzz::inf();
-  for (uint32_t i = threadIdx.x; i < chunks; i += 64) v.add(g1_xyzz::load(part + 32 * ((uint64_t)k * chunks + i)));
+  g1_acc29 v;
+  v.set_inf();
+  for (uint32_t i = threadIdx.x; i < chunks; i += 64)
+    v.add(g1_acc29::load_raw(part + (uint64_t)RAW29_WORDS * ((uint64_t)k * chunks + i)));
   uint32_t width = 1;
   while (width < chunks && width < 64) width <<= 1;
-  for (uint32_t m = width >> 1; m > 0; m >>= 1) v.add(shfl_xor_pt(v, m));
-  if (threadIdx.x == 0) v.store(T + 32 * (uint64_t)k);
+  for (uint32_t m = width >> 1; m > 0; m >>= 1) v.add(shfl_xor_acc(v, m));
+  if (threadIdx.x == 0) v.to_xyzz().store(T + 32 * (uint64_t)k);
 }
 
 // ------------------------------------------------------------------ driver (device part)
 void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* scalars, uint64_t N,
              uint32_t* T_out, hipEvent_t* ev) {
   // ev (optional, 5 events): [0] start, [1] after digits+sort, [2] after k_accumulate,
-  // [3] after run conversion + combine, [4] after bit-sum reduction
+  // [3] after combine, [4] after bit-sum reduction
   if (ev) hipEventRecord(ev[0], st);
   const int c = tb.c, W = tb.W;
   const uint32_t B = 1u << (c - 1);
@@ -674,26 +646,22 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   uint32_t* cnt = w.chunkcnt;
   const uint64_t lcap = nseg / CB_T + B + 16;
   hipMemsetAsync(cnt, 0, 4 * CB_LEVELS, st);
-  hipLaunchKernelGGL(k_accumulate, dim3(nb(nseg)), dim3(256), 0, st, w.bstart, w.segpart, w.segowner, w.chunklist,
-                     cnt, w.sorted, w.offsets, B + 1, tb.table, (uint32_t)L, w.raw29);
+  hipLaunchKernelGGL(k_accumulate, dim3(nb(nseg)), dim3(256), 0, st, w.segowner, w.chunklist, cnt, w.sorted,
+                     w.offsets, B + 1, tb.table, (uint32_t)L, w.raw29);
   if (ev) hipEventRecord(ev[2], st);  // the accumulate phase is the k_accumulate launch alone
-#ifndef KGS_ACC32
-  hipLaunchKernelGGL(k_raw29_convert, dim3(nb(B + 1 + nseg)), dim3(256), 0, st, w.bstart, w.segpart, w.raw29, B + 1,
-                     nseg);
-#endif
   uint64_t stride = 1, cap = lcap;
   for (int j = 0; j < CB_LEVELS; j++, stride *= CB_T) {
     uint32_t* lin = w.chunklist + (uint64_t)j * lcap;
     uint32_t* lout = j + 1 < CB_LEVELS ? w.chunklist + (uint64_t)(j + 1) * lcap : nullptr;
-    hipLaunchKernelGGL(k_combine_level, dim3(nb(cap)), dim3(256), 0, st, w.segpart, w.segowner, w.offsets, lin,
+    hipLaunchKernelGGL(k_combine_level, dim3(nb(cap)), dim3(256), 0, st, w.raw29, B + 1, w.segowner, w.offsets, lin,
                        cnt + j, lout, lout ? cnt + j + 1 : nullptr, (uint32_t)L, stride);
     cap = cap / CB_T + B + 16;
   }
-  hipLaunchKernelGGL(k_combine, dim3(nb(2 * (uint64_t)B)), dim3(256), 0, st, w.buckets, w.bstart, w.segpart,
-                     w.offsets, B, (uint32_t)L, stride);
+  hipLaunchKernelGGL(k_combine, dim3(nb(2 * (uint64_t)B)), dim3(256), 0, st, w.raw29, B + 1, w.offsets, B,
+                     (uint32_t)L, stride);
   if (ev) hipEventRecord(ev[3], st);
   const uint32_t chunks = (B / 2 + BS_SPAN - 1) / BS_SPAN > 0 ? (B / 2 + BS_SPAN - 1) / BS_SPAN : 1;
-  hipLaunchKernelGGL(k_bitsum1, dim3(chunks, c), dim3(256), 0, st, w.part, w.buckets, c, chunks);
+  hipLaunchKernelGGL(k_bitsum1, dim3(chunks, c), dim3(256), 0, st, w.part, w.raw29, c, chunks);
   hipLaunchKernelGGL(k_bitsum2, dim3(c), dim3(64), 0, st, T_out, w.part, chunks);
   if (ev) hipEventRecord(ev[4], st);
 }

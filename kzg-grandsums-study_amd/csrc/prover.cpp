@@ -308,16 +308,13 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
     w.counts = c.buf("msm_counts" + sfx, 4 * (B + 300));
     w.offsets = c.buf("msm_offsets" + sfx, 4 * (B + 4));
     w.cursor = c.buf("msm_cursor" + sfx, 4 * (B + 600));
-    w.bstart = c.buf("msm_bstart" + sfx, 128 * (size_t)(B + 2));
-    w.segpart = c.buf("msm_segpart" + sfx, 128 * nseg);
     w.segowner = c.buf("msm_segowner" + sfx, 4 * nseg);
     w.locnt = c.buf("msm_locnt" + sfx, 4 * 256 * 256 * 16);
     w.chunklist = c.buf("msm_chunklist" + sfx, 4 * 3 * (nseg / 16 + B + 16));
     w.chunkcnt = c.buf("msm_chunkcnt" + sfx, 64);
     w.raw29 = c.buf("msm_raw29" + sfx, 160 * ((size_t)B + 2 + nseg));
-    w.buckets = c.buf("msm_buckets" + sfx, 128 * (size_t)(B + 2));
     const uint32_t chunks = (B / 2 + 255) / 256 > 0 ? (B / 2 + 255) / 256 : 1;
-    w.part = c.buf("msm_part" + sfx, 128 * (size_t)cc * chunks);
+    w.part = c.buf("msm_part" + sfx, 160 * (size_t)cc * chunks);
   }
   c.srs_power = power;
   c.nbits_max = nbits_max;

@@ -142,6 +142,40 @@ def madd_bound(vb, legacy=False):
     return max(nX.val, Y3.val, ZZ3.val, ZZZ3.val)
 
 
+def add_bound(vb):
+    """g1_acc29::add (accumulator + accumulator, the combine / bit-sum trees) step by step"""
+    X1 = Y1 = ZZ1 = ZZZ1 = X2 = Y2 = ZZ2 = ZZZ2 = V(vb, MASK)
+    U1, U2, S1, S2 = _mul(X1, ZZ2), _mul(X2, ZZ1), _mul(Y1, ZZZ2), _mul(Y2, ZZZ1)
+    P = _norm(_sub(U2, U1, 8, 1))
+    R = _norm(_sub(S2, S1, 8, 1))
+    PP = _sqr(P)
+    assert PP.val <= 8 * Q                    # maybe_zero8's candidate set covers PP
+    PPP = _mul(P, PP)
+    ZZ3 = _mul(_mul(ZZ1, ZZ2), PP)
+    ZZZ3 = _mul(_mul(ZZZ1, ZZZ2), PPP)
+    Qv = _mul(U1, PP)
+    R2 = _sqr(R)
+    nX = _norm(_sub(R2, _add(PPP, _add(Qv, Qv)), 16, 3))
+    T = _sub(Qv, nX, 64, 1)
+    Y3 = _mul2(R, T, S1, _neg(PPP, 3, 1))
+    for c in (P, R, nX, Y3, ZZ3, ZZZ3):
+        assert _mul(c, V(Q, MASK)).val <= 2 * Q
+    return max(nX.val, Y3.val, ZZ3.val, ZZZ3.val)
+
+
+def test_full_add_bounds():
+    # the tree adds take two accumulators from the bucket chains (< vb) and must stay below vb;
+    # from_xyzz (doubling path) yields < 2q
+    vb = 2 * Q
+    for _ in range(50):
+        nxt = max(madd_bound(vb), vb)
+        if nxt == vb:
+            break
+        vb = nxt
+    assert add_bound(vb) <= vb
+    assert 2 * Q <= vb
+
+
 @pytest.mark.parametrize("legacy", [False, True])
 def test_add_aff_bounds_fixed_point(legacy):
     # initial accumulator: a table point (< q) with ZZ = ZZZ = 2^261 mod q; negated y: 2q - y
@@ -158,7 +192,8 @@ def test_add_aff_bounds_fixed_point(legacy):
 def test_spread_constants_used_by_header():
     t = _hdr()
     uses = set(re.findall(r"(?:sub|neg)<(\d+), (\d+)>", t))
-    assert uses == {("30", "1"), ("32", "2"), ("16", "3"), ("64", "1"), ("16", "1"), ("2", "1"), ("3", "1")}
+    assert uses == {("30", "1"), ("32", "2"), ("16", "3"), ("64", "1"), ("16", "1"), ("2", "1"), ("3", "1"),
+                    ("8", "1")}
     for k, s in uses:
         _spread(int(k), int(s))
     # the initial negation 2q - y of a canonical y (< q) stays nonnegative per limb
