@@ -35,7 +35,7 @@ struct MsmWork {
   uint8_t* lo = nullptr;
   uint32_t* blockhist = nullptr;  // (NH <= 264) x ceil(N/256) per-block partition counts
   uint32_t *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *sorted = nullptr;
-  uint32_t* part = nullptr;      // bit-sum chunk partials (c x chunks run records)
+  uint32_t* part = nullptr;      // bucket row + column sums (2^h + 2^l run records, msm.hip k_rowcol)
   uint32_t* segowner = nullptr;  // bucket of each segment's first run
   uint32_t* locnt = nullptr;     // lo pass: 256 partitions x 256 lo x 16 chunks counts / bases
   uint32_t* chunklist = nullptr; // combine levels: 3 lists of chunk-start segments

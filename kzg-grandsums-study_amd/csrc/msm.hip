@@ -526,68 +526,64 @@ __global__ void __launch_bounds__(256) k_combine(uint32_t* __restrict__ raw, uin
 }
 
 // ------------------------------------------------------------------ sum_b b*S_b via bit sums
-// T_k = sum of the buckets b in [1, B-1] with bit k set (k < c-1; the t-th such bucket: insert a
-// 1 at bit k of t), T_{c-1} = S_B. Block (chunk, k): every thread first adds BS_CHAIN buckets in
-// sequence (all lanes busy), then one LDS tree over the 256 thread sums (the active lanes stay
-// packed in the low waves, so the tree costs ~9 wave-adds instead of 6 per wave with shuffles).
-#ifndef KGS_BS_CHAIN
-#define KGS_BS_CHAIN 8
-#endif
-constexpr int BS_CHAIN = KGS_BS_CHAIN;
-constexpr uint32_t BS_SPAN = 256 * BS_CHAIN;  // buckets per block
-
-__device__ __forceinline__ g1_acc29 block_tree_sum256(g1_acc29 v, uint32_t* lds) {
-  for (int stride = 128; stride > 0; stride >>= 1) {
-    if (threadIdx.x >= stride && threadIdx.x < 2 * stride) v.store_raw(lds + RAW29_WORDS * (threadIdx.x - stride));
+// Write a bucket index b < B = 2^(c-1) as b = hi*2^l + lo (l = ceil((c-1)/2) low bits, h = c-1-l
+// high bits). Then sum_{b<B} b*S_b = 2^l * sum_hi hi*Row_hi + sum_lo lo*Col_lo with the row sums
+// Row_hi = sum_lo S_{hi,lo} and column sums Col_lo = sum_hi S_{hi,lo}, and each of those is a bit sum:
+// sum_hi hi*Row_hi = sum_j 2^j TR_j, TR_j = sum_{hi with bit j} Row_hi (likewise TC_k). Hence the c
+// bit sums the host's Horner step expects are T_k = TC_k (k < l), T_{l+j} = TR_j (j < h) and
+// T_{c-1} = S_B. Work: 2B adds for the row/column sums + c*2^(l-1) for the bit sums (c = 17: 0.13 M
+// adds instead of the (c-1)*B/2 = 0.52 M of summing every bucket once per set bit), at the minimal
+// depth of log2(B/2) + 1 dependent adds.
+// k_rowcol: block r < 2^h sums row r, block 2^h + r sums column r; one element per thread, LDS tree.
+__device__ __forceinline__ g1_acc29 block_tree_sum(g1_acc29 v, uint32_t* lds) {
+  for (int stride = blockDim.x >> 1; stride > 0; stride >>= 1) {
+    if ((int)threadIdx.x >= stride && (int)threadIdx.x < 2 * stride)
+      v.store_raw(lds + RAW29_WORDS * (threadIdx.x - stride));
     __syncthreads();
-    if (threadIdx.x < stride) v.add(g1_acc29::load_raw(lds + RAW29_WORDS * threadIdx.x));
+    if ((int)threadIdx.x < stride) v.add(g1_acc29::load_raw(lds + RAW29_WORDS * threadIdx.x));
     __syncthreads();
   }
   return v;
 }
 
-// part: c x chunks run records; the bucket totals are run_rec(raw, b)
-__global__ void __launch_bounds__(256) k_bitsum1(uint32_t* __restrict__ part, const uint32_t* __restrict__ raw,
-                                                 int c, uint32_t chunks) {
+__global__ void __launch_bounds__(256) k_rowcol(uint32_t* __restrict__ rc, const uint32_t* __restrict__ raw, int c) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[128 * RAW29_WORDS];
-  const int k = blockIdx.y;
-  const uint32_t chunk = blockIdx.x;
-  const uint32_t B = 1u << (c - 1);
+  const int l = c / 2, h = c - 1 - l;  // l = ceil((c-1)/2)
+  const uint32_t r = blockIdx.x, t = threadIdx.x;
+  const bool row = r < (1u << h);
+  g1_acc29 v;
+  v.set_inf();
+  const uint32_t n = row ? 1u << l : 1u << h;  // elements of this row / column (<= 256)
+  if (t < n) {
+    const uint32_t b = row ? (r << l) | t : (t << l) | (r - (1u << h));
+    if (b) v = g1_acc29::load_raw(run_rec(raw, b));
+  }
+  v = block_tree_sum(v, lds);
+  if (t == 0) v.store_raw(rc + (uint64_t)RAW29_WORDS * r);
+}
+
+// one block per k < c: T_k = sum of the column sums with bit k set (k < l), of the row sums with bit
+// k - l set (l <= k < c-1), or S_B (k = c-1); 256-bit XYZZ out for the host
+__global__ void __launch_bounds__(128) k_bitsum_rc(uint32_t* __restrict__ T, const uint32_t* __restrict__ rc,
+                                                   const uint32_t* __restrict__ raw, int c) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[64 * RAW29_WORDS];
+  const int l = c / 2, h = c - 1 - l;
+  const int k = blockIdx.x;
+  const uint32_t t = threadIdx.x;
   g1_acc29 v;
   v.set_inf();
   if (k == c - 1) {
-    if (chunk == 0 && threadIdx.x == 0) v = g1_acc29::load_raw(run_rec(raw, B));
+    if (t == 0) v = g1_acc29::load_raw(run_rec(raw, 1u << (c - 1)));
   } else {
-#pragma unroll 1
-    for (int i = 0; i < BS_CHAIN; i++) {
-      const uint32_t t = chunk * BS_SPAN + i * 256 + threadIdx.x;
-      if (t < B / 2) {
-        const uint32_t b = ((t >> k) << (k + 1)) | (1u << k) | (t & ((1u << k) - 1));
-        v.add(g1_acc29::load_raw(run_rec(raw, b)));
-      }
+    const int bits = k < l ? l : h, j = k < l ? k : k - l;  // sum over 2^(bits-1) entries <= 128
+    const uint32_t base = k < l ? 1u << h : 0u;             // column sums follow the row sums
+    if (t < (1u << (bits - 1))) {
+      const uint32_t idx = ((t >> j) << (j + 1)) | (1u << j) | (t & ((1u << j) - 1));
+      v = g1_acc29::load_raw(rc + (uint64_t)RAW29_WORDS * (base + idx));
     }
   }
-  uint32_t* out = part + (uint64_t)RAW29_WORDS * ((uint64_t)k * chunks + chunk);
-  if (k == c - 1 && chunk > 0) {  // uniform per block: an empty partial
-    if (threadIdx.x == 0) v.store_raw(out);
-    return;
-  }
-  v = block_tree_sum256(v, lds);
-  if (threadIdx.x == 0) v.store_raw(out);
-}
-
-// one wave per k: sum the chunk partials (<= 64 per lane pass), xor-shuffle tree, 256-bit XYZZ out
-__global__ void __launch_bounds__(64) k_bitsum2(uint32_t* __restrict__ T, const uint32_t* __restrict__ part,
-                                                uint32_t chunks) {
-  const int k = blockIdx.x;
-  g1_acc29 v;
-  v.set_inf();
-  for (uint32_t i = threadIdx.x; i < chunks; i += 64)
-    v.add(g1_acc29::load_raw(part + (uint64_t)RAW29_WORDS * ((uint64_t)k * chunks + i)));
-  uint32_t width = 1;
-  while (width < chunks && width < 64) width <<= 1;
-  for (uint32_t m = width >> 1; m > 0; m >>= 1) v.add(shfl_xor_acc(v, m));
-  if (threadIdx.x == 0) v.to_xyzz().store(T + 32 * (uint64_t)k);
+  v = block_tree_sum(v, lds);
+  if (t == 0) v.to_xyzz().store(T + 32 * (uint64_t)k);
 }
 
 // ------------------------------------------------------------------ driver (device part)
@@ -660,9 +656,9 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   hipLaunchKernelGGL(k_combine, dim3(nb(2 * (uint64_t)B)), dim3(256), 0, st, w.raw29, B + 1, w.offsets, B,
                      (uint32_t)L, stride);
   if (ev) hipEventRecord(ev[3], st);
-  const uint32_t chunks = (B / 2 + BS_SPAN - 1) / BS_SPAN > 0 ? (B / 2 + BS_SPAN - 1) / BS_SPAN : 1;
-  hipLaunchKernelGGL(k_bitsum1, dim3(chunks, c), dim3(256), 0, st, w.part, w.raw29, c, chunks);
-  hipLaunchKernelGGL(k_bitsum2, dim3(c), dim3(64), 0, st, T_out, w.part, chunks);
+  // row / column sums (2^h + 2^l blocks), then the c bit sums
+  hipLaunchKernelGGL(k_rowcol, dim3((1u << (c - 1 - c / 2)) + (1u << (c / 2))), dim3(256), 0, st, w.part, w.raw29, c);
+  hipLaunchKernelGGL(k_bitsum_rc, dim3(c), dim3(128), 0, st, T_out, w.part, w.raw29, c);
   if (ev) hipEventRecord(ev[4], st);
 }
 

@@ -313,8 +313,7 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
     w.chunklist = c.buf("msm_chunklist" + sfx, 4 * 3 * (nseg / 16 + B + 16));
     w.chunkcnt = c.buf("msm_chunkcnt" + sfx, 64);
     w.raw29 = c.buf("msm_raw29" + sfx, 160 * ((size_t)B + 2 + nseg));
-    const uint32_t chunks = (B / 2 + 255) / 256 > 0 ? (B / 2 + 255) / 256 : 1;
-    w.part = c.buf("msm_part" + sfx, 160 * (size_t)cc * chunks);
+    w.part = c.buf("msm_part" + sfx, 160 * (size_t)(2 << (cc / 2)));  // row + column sums
   }
   c.srs_power = power;
   c.nbits_max = nbits_max;
