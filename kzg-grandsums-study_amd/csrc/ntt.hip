@@ -131,6 +131,156 @@ __global__ void __launch_bounds__(256) k_ntt_dit_pass(uint32_t* __restrict__ dat
 
 static inline unsigned nblocks(uint64_t work, unsigned bs = 256) { return (unsigned)((work + bs - 1) / bs); }
 
+// ---------------------------------------------------------------- LDS-staged passes (K1 + K2 stages)
+// The same butterflies with the same stage twiddles as the radix-8 passes above (so the output is
+// bit-identical), but K = K1 + K2 <= 6 stages per global read/write of the data: a block stages
+// LDS_ELEMS = 2048 elements (64 KB) in LDS, runs a radix-2^K1 register round, exchanges through LDS,
+// runs a radix-2^K2 round, and writes back. An m = 2^21 transform takes 4 passes instead of 7.
+// Index map of a pass (group stride d = 2^logd; DIF: logd = logm - s0 - K, DIT: logd = s0):
+// idx(col, j) = (hi << (logd + K)) | (j << logd) | lo, col = (hi << logd) | lo, j < 2^K. Block b owns
+// columns [b*LB, (b+1)*LB), LB = 2048 >> K; its elements are contiguous runs of min(LB, d) (logd >=
+// log2 LB) or 2^(logd+K) (otherwise) elements, loaded and stored in address order (coalesced). LDS
+// layout: element (j, col - b*LB) at lds[(j * LB + cl) * 8].
+constexpr int LDS_ELEMS = 2048;
+
+__device__ __forceinline__ void lds_map(uint32_t e, int K, int logd, int lblog, uint32_t& j, uint32_t& cl) {
+  if (logd >= lblog) {  // for each j a run of LB consecutive lo
+    j = e >> lblog;
+    cl = e & ((1u << lblog) - 1);
+  } else {              // contiguous hi blocks of 2^(logd + K) elements
+    const uint32_t lo = e & ((1u << logd) - 1);
+    j = (e >> logd) & ((1u << K) - 1);
+    cl = ((e >> (logd + K)) << logd) | lo;
+  }
+}
+
+__device__ __forceinline__ uint64_t lds_idx(uint64_t col, uint32_t j, int K, int logd) {
+  const uint64_t lo = col & ((1ull << logd) - 1), hi = col >> logd;
+  return (hi << (logd + K)) | ((uint64_t)j << logd) | lo;
+}
+
+// one register round of R stages of a pass on the 2^R elements j = jb + js * r (r < 2^R) of column
+// col: stage k of the round is pass stage kp0 + k; DIF pairs (r, r + 2^(R-1-k)), DIT (r, r + 2^k)
+template <int R, bool DIT>
+__device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restrict__ tw, uint32_t cl, uint64_t col,
+                                          uint32_t jb, uint32_t js, int K, int logd, int lb, int kp0) {
+  fr x[1 << R];
+#pragma unroll
+  for (int r = 0; r < (1 << R); r++) x[r] = fr::load(lds + 8 * ((jb + js * r) * lb + cl));
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    const int kp = kp0 + k;                                 // stage within the pass
+    const int logh = DIT ? logd + kp : logd + K - 1 - kp;   // half-distance h = 2^logh
+    const int dist = DIT ? 1 << k : 1 << (R - 1 - k);       // register distance
+#pragma unroll
+    for (int q = 0; q < (1 << (R - 1)); q++) {
+      const int r = ((q / dist) * 2 * dist) + (q % dist);
+      const uint64_t idx = lds_idx(col, jb + js * r, K, logd);
+      const uint64_t t = idx & ((1ull << logh) - 1);
+      const uint32_t* w = tw + 8 * ((1ull << logh) + t);  // stage table: w_{2h}^t = tw[h + t]
+      fr a = x[r], b = x[r + dist];
+      if (DIT) {
+        if (t) b = b * fr::load(w);
+        x[r] = a + b;
+        x[r + dist] = a - b;
+      } else {
+        x[r] = a + b;
+        fr diff = a - b;
+        if (t) diff = diff * fr::load(w);
+        x[r + dist] = diff;
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < (1 << R); r++) x[r].store(lds + 8 * ((jb + js * r) * lb + cl));
+}
+
+// K1 + K2 stages from s0. in: first-pass source (DIF: zero beyond in_len, times pre[idx]; DIT: gathered
+// through bit reversal unless in_bitrev); post / post_s: last-pass multipliers (DIT).
+template <int K1, int K2, bool DIT>
+__global__ void __launch_bounds__(256) k_ntt_lds_pass(uint32_t* __restrict__ data, const uint32_t* __restrict__ in,
+                                                      uint64_t in_len, int in_bitrev, const uint32_t* __restrict__ pre,
+                                                      const uint32_t* __restrict__ tw, int logm, int s0,
+                                                      const uint32_t* __restrict__ post,
+                                                      const uint32_t* __restrict__ post_s) {
+  constexpr int K = K1 + K2;
+  constexpr int LBLOG = 11 - K;
+  constexpr int LB = 1 << LBLOG;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_ELEMS * 8];
+  const int logd = DIT ? s0 : logm - s0 - K;
+  const uint64_t col0 = (uint64_t)blockIdx.x * LB;
+  // load (address order)
+  for (uint32_t e = threadIdx.x; e < LDS_ELEMS; e += 256) {
+    uint32_t j, cl;
+    lds_map(e, K, logd, LBLOG, j, cl);
+    const uint64_t idx = lds_idx(col0 + cl, j, K, logd);
+    fr x;
+    if (in) {
+      if (DIT) {
+        x = fr::load(in + 8 * (in_bitrev ? idx : (uint64_t)bitrev((uint32_t)idx, logm)));
+      } else if (idx < in_len) {
+        x = fr::load(in + 8 * idx);
+        if (pre) x = x * fr::load(pre + 8 * idx);
+      } else {
+        x = fr::zero();
+      }
+    } else {
+      x = fr::load(data + 8 * idx);
+    }
+    x.store(lds + 8 * (j * LB + cl));
+  }
+  __syncthreads();
+  // round 1: DIF pairs at j-distances 2^(K-1) .. 2^K2 (j = jl + 2^K2 r); DIT 1 .. 2^(K1-1) (j = 2^K1 jh + r)
+  for (uint32_t g = threadIdx.x; g < (LDS_ELEMS >> K1); g += 256) {
+    const uint32_t cl = g & (LB - 1), jq = g >> LBLOG;
+    if (DIT)
+      lds_round<K1, true>(lds, tw, cl, col0 + cl, jq << K1, 1, K, logd, LB, 0);
+    else
+      lds_round<K1, false>(lds, tw, cl, col0 + cl, jq, 1u << K2, K, logd, LB, 0);
+  }
+  __syncthreads();
+  // round 2: DIF j-distances 2^(K2-1) .. 1 (j = 2^K2 jh + r); DIT 2^K1 .. 2^(K-1) (j = jl + 2^K1 r)
+  for (uint32_t g = threadIdx.x; g < (LDS_ELEMS >> K2); g += 256) {
+    const uint32_t cl = g & (LB - 1), jq = g >> LBLOG;
+    if (DIT)
+      lds_round<K2, true>(lds, tw, cl, col0 + cl, jq, 1u << K1, K, logd, LB, K1);
+    else
+      lds_round<K2, false>(lds, tw, cl, col0 + cl, jq << K2, 1, K, logd, LB, K1);
+  }
+  __syncthreads();
+  fr ps;
+  if (post_s) ps = fr::load(post_s);
+  for (uint32_t e = threadIdx.x; e < LDS_ELEMS; e += 256) {
+    uint32_t j, cl;
+    lds_map(e, K, logd, LBLOG, j, cl);
+    const uint64_t idx = lds_idx(col0 + cl, j, K, logd);
+    fr y = fr::load(lds + 8 * (j * LB + cl));
+    if (post) y = y * fr::load(post + 8 * idx);
+    if (post_s) y = y * ps;
+    y.store(data + 8 * idx);
+  }
+}
+
+#ifndef KGS_NO_NTT_LDS
+// stages per pass for m = 2^logm: LDS passes of up to 6 stages while >= 4 remain, radix-8/4/2 after
+static inline int lds_pass_stages(int left) { return left >= 6 ? 6 : left >= 4 ? left : 0; }
+
+static void launch_lds_pass(hipStream_t st, int K, bool dit, uint32_t* data, const uint32_t* in, uint64_t in_len,
+                            int in_bitrev, const uint32_t* pre, const uint32_t* tw, int logm, int s0,
+                            const uint32_t* post, const uint32_t* post_s) {
+  const unsigned blocks = (unsigned)((1ull << logm) / LDS_ELEMS);
+#define KGS_LDS_LAUNCH(A, B, D)                                                                                  \
+  hipLaunchKernelGGL((k_ntt_lds_pass<A, B, D>), dim3(blocks), dim3(256), 0, st, data, in, in_len, in_bitrev, pre, \
+                     tw, logm, s0, post, post_s)
+  if (dit) {
+    if (K == 6) KGS_LDS_LAUNCH(3, 3, true); else if (K == 5) KGS_LDS_LAUNCH(3, 2, true); else KGS_LDS_LAUNCH(2, 2, true);
+  } else {
+    if (K == 6) KGS_LDS_LAUNCH(3, 3, false); else if (K == 5) KGS_LDS_LAUNCH(3, 2, false); else KGS_LDS_LAUNCH(2, 2, false);
+  }
+#undef KGS_LDS_LAUNCH
+}
+#endif
+
 void ntt_dif(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t in_len, int logm,
              const uint32_t* pre, const uint32_t* tw, int logM) {
   if (logm == 0) {
@@ -144,10 +294,19 @@ void ntt_dif(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t in_len,
   int s0 = 0;
   bool first = true;
   while (s0 < logm) {
-    int K = logm - s0 >= 3 ? 3 : logm - s0;
-    uint64_t groups = (1ull << logm) >> K;
     const uint32_t* src = first ? in : nullptr;
     const uint32_t* p = first ? pre : nullptr;
+#ifndef KGS_NO_NTT_LDS
+    const int KL = logm >= 11 ? lds_pass_stages(logm - s0) : 0;
+    if (KL) {
+      launch_lds_pass(st, KL, false, out, src, in_len, 1, p, tw, logm, s0, nullptr, nullptr);
+      s0 += KL;
+      first = false;
+      continue;
+    }
+#endif
+    int K = logm - s0 >= 3 ? 3 : logm - s0;
+    uint64_t groups = (1ull << logm) >> K;
     if (K == 3)
       hipLaunchKernelGGL(k_ntt_dif_pass<3>, dim3(nblocks(groups)), dim3(256), 0, st, out, src, in_len, p, tw, logM, logm, s0);
     else if (K == 2)
@@ -165,15 +324,28 @@ void ntt_dit(hipStream_t st, uint32_t* out, const uint32_t* in, int in_bitrev, i
     launch_scale_copy(st, out, in, 1, post, post_s);
     return;
   }
-  // passes: the first pass handles the remainder so the last pass is a full radix-8 one
+  // passes: LDS passes of up to 6 stages while >= 4 stages remain (m >= 2048), then radix-8/4/2
+  // passes; otherwise the first pass handles the remainder so the last pass is a full radix-8 one
   int rem = logm % 3;
   int s0 = 0;
   bool first = true;
   while (s0 < logm) {
+    const uint32_t* src = first ? in : nullptr;
+#ifndef KGS_NO_NTT_LDS
+    const int KL = logm >= 11 ? lds_pass_stages(logm - s0) : 0;
+    if (KL) {
+      const bool last = s0 + KL == logm;
+      launch_lds_pass(st, KL, true, out, src, 0, in_bitrev, nullptr, tw, logm, s0, last ? post : nullptr,
+                      last ? post_s : nullptr);
+      s0 += KL;
+      first = false;
+      continue;
+    }
+    if (logm >= 11) rem = 0;
+#endif
     int K = first && rem ? rem : 3;
     if (K > logm - s0) K = logm - s0;
     uint64_t groups = (1ull << logm) >> K;
-    const uint32_t* src = first ? in : nullptr;
     bool last = s0 + K == logm;
     const uint32_t* p = last ? post : nullptr;
     const uint32_t* ps = last ? post_s : nullptr;
