@@ -127,33 +127,36 @@ struct fq29 {
     return r;
   }
 
+  // CIOS output: 9 64-bit columns before the final carry pass (value = sum_j t_j 2^(29 j)). The
+  // consumers either run the carry pass alone (carry) or fold an addition of a spread constant into it
+  // (carry_sub): one normalisation instead of two where a product feeds a sum or difference.
+  struct cols {
+    uint64_t t[9];
+  };
+  // CIOS reduction step after row i's partial products: t += m*q (m = -t0/q mod 2^29), shift down
+  __device__ __forceinline__ static void reduce_row(uint64_t (&t)[9]) {
+    const uint32_t m = ((uint32_t)t[0] * f29::INV) & f29::MASK;
+    const uint64_t c = ((uint64_t)m * f29::Q.v[0] + t[0]) >> 29;
+#pragma unroll
+    for (int j = 1; j < 9; j++) t[j] = (uint64_t)m * f29::Q.v[j] + t[j];
+#pragma unroll
+    for (int j = 0; j < 8; j++) t[j] = t[j + 1];
+    t[0] += c;
+    t[8] = 0;
+  }
+
   // Montgomery product a*b*2^-261 (CIOS, 64-bit column accumulators, no carry words).
   // Needs 9*max(a_j)*max(b_j) + 9*(2^29)^2 + 2^36 < 2^64 (e.g. a_j < 2^29, b_j < 2^30.6) and
-  // a*b < 2^261 * (2^261 - q); the result is normalised and < a*b/2^261 + q.
-  __device__ __forceinline__ static fq29 mul(const fq29& a, const fq29& b) {
-    uint64_t t[9];
+  // a*b < 2^261 * (2^261 - q); the result is < a*b/2^261 + q.
+  __device__ __forceinline__ static cols mul_cols(const fq29& a, const fq29& b) {
+    cols r;
 #pragma unroll
-    for (int j = 0; j < 9; j++) t[j] = 0;
+    for (int j = 0; j < 9; j++) r.t[j] = 0;
 #pragma unroll
     for (int i = 0; i < 9; i++) {
 #pragma unroll
-      for (int j = 0; j < 9; j++) t[j] = (uint64_t)a.l[i] * b.l[j] + t[j];
-      const uint32_t m = ((uint32_t)t[0] * f29::INV) & f29::MASK;
-      const uint64_t c = ((uint64_t)m * f29::Q.v[0] + t[0]) >> 29;
-#pragma unroll
-      for (int j = 1; j < 9; j++) t[j] = (uint64_t)m * f29::Q.v[j] + t[j];
-#pragma unroll
-      for (int j = 0; j < 8; j++) t[j] = t[j + 1];
-      t[0] += c;
-      t[8] = 0;
-    }
-    fq29 r;
-    uint64_t c = 0;
-#pragma unroll
-    for (int j = 0; j < 9; j++) {
-      const uint64_t s = t[j] + c;
-      r.l[j] = (uint32_t)s & f29::MASK;
-      c = s >> 29;
+      for (int j = 0; j < 9; j++) r.t[j] = (uint64_t)a.l[i] * b.l[j] + r.t[j];
+      reduce_row(r.t);
     }
     return r;
   }
@@ -162,69 +165,74 @@ struct fq29 {
   // once (2a_i * a_j, j > i, and a_i^2 on the diagonal): 45 + 81 mads instead of 162. Row i adds to
   // absolute columns 2i..i+8, which sit at t[i..8] after i shifts. A column receives at most 5
   // products (<= 2 * max(a_j)^2 each), so it stays below mul's bound for a normalised a.
-  __device__ __forceinline__ static fq29 sqr(const fq29& a) {
+  __device__ __forceinline__ static cols sqr_cols(const fq29& a) {
     uint32_t d[9];
 #pragma unroll
     for (int j = 0; j < 9; j++) d[j] = a.l[j] << 1;
-    uint64_t t[9];
+    cols r;
 #pragma unroll
-    for (int j = 0; j < 9; j++) t[j] = 0;
+    for (int j = 0; j < 9; j++) r.t[j] = 0;
 #pragma unroll
     for (int i = 0; i < 9; i++) {
-      t[i] = (uint64_t)a.l[i] * a.l[i] + t[i];
+      r.t[i] = (uint64_t)a.l[i] * a.l[i] + r.t[i];
 #pragma unroll
-      for (int j = i + 1; j < 9; j++) t[j] = (uint64_t)d[i] * a.l[j] + t[j];
-      const uint32_t m = ((uint32_t)t[0] * f29::INV) & f29::MASK;
-      const uint64_t c = ((uint64_t)m * f29::Q.v[0] + t[0]) >> 29;
-#pragma unroll
-      for (int j = 1; j < 9; j++) t[j] = (uint64_t)m * f29::Q.v[j] + t[j];
-#pragma unroll
-      for (int j = 0; j < 8; j++) t[j] = t[j + 1];
-      t[0] += c;
-      t[8] = 0;
+      for (int j = i + 1; j < 9; j++) r.t[j] = (uint64_t)d[i] * a.l[j] + r.t[j];
+      reduce_row(r.t);
     }
+    return r;
+  }
+
+  // (a*b + c*d)*2^-261 with ONE Montgomery reduction (lazy reduction of a sum of products): each CIOS
+  // row adds both rows of partial products before its reduction step, 243 mads instead of 324.
+  // Needs 9*(max a_j * max b_j + max c_j * max d_j) + 9*(2^29)^2 + 2^36 < 2^64 (a and c normalised)
+  // and a*b + c*d < 2^261 * (2^261 - q); the result is < (a*b + c*d)/2^261 + q.
+  __device__ __forceinline__ static cols mul2_cols(const fq29& a, const fq29& b, const fq29& c2, const fq29& d2) {
+    cols r;
+#pragma unroll
+    for (int j = 0; j < 9; j++) r.t[j] = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+#pragma unroll
+      for (int j = 0; j < 9; j++) r.t[j] = (uint64_t)a.l[i] * b.l[j] + r.t[j];
+#pragma unroll
+      for (int j = 0; j < 9; j++) r.t[j] = (uint64_t)c2.l[i] * d2.l[j] + r.t[j];
+      reduce_row(r.t);
+    }
+    return r;
+  }
+
+  // final carry pass: normalised limbs
+  __device__ __forceinline__ static fq29 carry(const cols& x) {
     fq29 r;
     uint64_t c = 0;
 #pragma unroll
     for (int j = 0; j < 9; j++) {
-      const uint64_t s = t[j] + c;
+      const uint64_t s = x.t[j] + c;
       r.l[j] = (uint32_t)s & f29::MASK;
       c = s >> 29;
     }
     return r;
   }
-  // (a*b + c*d)*2^-261 with ONE Montgomery reduction (lazy reduction of a sum of products): each CIOS
-  // row adds both rows of partial products before its reduction step, 243 mads instead of 324.
-  // Needs 9*(max a_j * max b_j + max c_j * max d_j) + 9*(2^29)^2 + 2^36 < 2^64 (all four normalised)
-  // and a*b + c*d < 2^261 * (2^261 - q); the result is normalised and < (a*b + c*d)/2^261 + q.
-  __device__ __forceinline__ static fq29 mul2(const fq29& a, const fq29& b, const fq29& c2, const fq29& d2) {
-    uint64_t t[9];
-#pragma unroll
-    for (int j = 0; j < 9; j++) t[j] = 0;
-#pragma unroll
-    for (int i = 0; i < 9; i++) {
-#pragma unroll
-      for (int j = 0; j < 9; j++) t[j] = (uint64_t)a.l[i] * b.l[j] + t[j];
-#pragma unroll
-      for (int j = 0; j < 9; j++) t[j] = (uint64_t)c2.l[i] * d2.l[j] + t[j];
-      const uint32_t m = ((uint32_t)t[0] * f29::INV) & f29::MASK;
-      const uint64_t c = ((uint64_t)m * f29::Q.v[0] + t[0]) >> 29;
-#pragma unroll
-      for (int j = 1; j < 9; j++) t[j] = (uint64_t)m * f29::Q.v[j] + t[j];
-#pragma unroll
-      for (int j = 0; j < 8; j++) t[j] = t[j + 1];
-      t[0] += c;
-      t[8] = 0;
-    }
+  // norm(x + K - b) in ONE carry pass (K = spread(k, s): every limb of K >= b's limb; x's columns
+  // < 2^63, read as int64)
+  template <uint32_t K, uint32_t S>
+  __device__ __forceinline__ static fq29 carry_sub(const cols& x, const fq29& b) {
+    constexpr f29::L9 Kc = f29::spread(K, S);
     fq29 r;
-    uint64_t c = 0;
+    int64_t c = 0;
 #pragma unroll
     for (int j = 0; j < 9; j++) {
-      const uint64_t s = t[j] + c;
-      r.l[j] = (uint32_t)s & f29::MASK;
+      const int64_t s = (int64_t)(Kc.v[j] - b.l[j]) + (int64_t)x.t[j] + c;
+      r.l[j] = j < 8 ? ((uint32_t)s & f29::MASK) : (uint32_t)s;
       c = s >> 29;
     }
     return r;
+  }
+
+  __device__ __forceinline__ static fq29 mul(const fq29& a, const fq29& b) { return carry(mul_cols(a, b)); }
+  __device__ __forceinline__ static fq29 sqr(const fq29& a) { return carry(sqr_cols(a)); }
+  __device__ __forceinline__ static fq29 mul2(const fq29& a, const fq29& b, const fq29& c2, const fq29& d2) {
+    return carry(mul2_cols(a, b, c2, d2));
   }
 
   // necessary condition for "== 0 mod q" of a normalised value < 8q: its low limb is (j*q) mod 2^29
@@ -272,19 +280,15 @@ struct g1_acc29 {
       inf = false;
       return;
     }
-    const fq29 U2 = fq29::mul(x2, ZZ);
+    // P = U2 - X1 with the product's carry pass folded into the difference's normalisation
+    const fq29 P = fq29::carry_sub<30, 1>(fq29::mul_cols(x2, ZZ), X);
     const fq29 S2 = fq29::mul(y2, ZZZ);
-    const fq29 P = fq29::sub<30, 1>(U2, X).norm();
     // R = S2 - Y1, or -S2 - Y1 for a negated point: K - Y1 +- S2 (limbs of K - Y1 >= 2^30 > S2's)
     fq29 R = fq29::neg<32, 2>(Y);
 #pragma unroll
     for (int j = 0; j < 9; j++) R.l[j] = negy ? R.l[j] - S2.l[j] : R.l[j] + S2.l[j];
     R = R.norm();
-#ifndef KGS_NO_SQR29
     const fq29 PP = fq29::sqr(P);  // < 6.8 q
-#else
-    const fq29 PP = fq29::mul(P, P);
-#endif
     if (PP.maybe_zero8()) {  // rare: decide exactly
       if (P.to_fq().is_zero()) {
         if (R.to_fq().is_zero()) {  // same point: doubling (256-bit path, converted back)
@@ -303,29 +307,16 @@ struct g1_acc29 {
         return;
       }
     }
-#ifndef KGS_NO_SQR29
     // ordered so that P, PP, ZZ, ZZZ and Qv die early: mul2 below has four operands live, and at
     // <= 168 VGPRs the kernel keeps 3 waves per SIMD without spilling
     const fq29 PPP = fq29::mul(P, PP);
     ZZ = fq29::mul(ZZ, PP);
     const fq29 Qv = fq29::mul(X, PP);
     ZZZ = fq29::mul(ZZZ, PPP);
-    const fq29 R2 = fq29::sqr(R);
-    X = fq29::sub<16, 3>(R2, fq29::add(PPP, fq29::add(Qv, Qv))).norm();
+    X = fq29::sub<16, 3>(fq29::sqr(R), fq29::add(PPP, fq29::add(Qv, Qv))).norm();
     const fq29 T = fq29::sub<64, 1>(Qv, X);
     // Y3 = R*T - Y1*PPP = R*T + Y1*(3q - PPP) mod q, one reduction (PPP < 2.3q)
     Y = fq29::mul2(R, T, Y, fq29::neg<3, 1>(PPP));
-#else
-    const fq29 PPP = fq29::mul(P, PP);
-    const fq29 Qv = fq29::mul(X, PP);
-    const fq29 R2 = fq29::mul(R, R);
-    const fq29 nX = fq29::sub<16, 3>(R2, fq29::add(PPP, fq29::add(Qv, Qv))).norm();
-    const fq29 T = fq29::sub<64, 1>(Qv, nX);
-    Y = fq29::sub<16, 1>(fq29::mul(R, T), fq29::mul(Y, PPP)).norm();
-    X = nX;
-    ZZ = fq29::mul(ZZ, PP);
-    ZZZ = fq29::mul(ZZZ, PPP);
-#endif
   }
 
   // this += o, both accumulators (add-2008-s; coordinates < 2^258.6, normalised): the bucket
@@ -341,11 +332,9 @@ struct g1_acc29 {
       return;
     }
     const fq29 U1 = fq29::mul(X, o.ZZ);
-    const fq29 U2 = fq29::mul(o.X, ZZ);
     const fq29 S1 = fq29::mul(Y, o.ZZZ);
-    const fq29 S2 = fq29::mul(o.Y, ZZZ);
-    const fq29 P = fq29::sub<8, 1>(U2, U1).norm();
-    const fq29 R = fq29::sub<8, 1>(S2, S1).norm();
+    const fq29 P = fq29::carry_sub<8, 1>(fq29::mul_cols(o.X, ZZ), U1);   // U2 - U1
+    const fq29 R = fq29::carry_sub<8, 1>(fq29::mul_cols(o.Y, ZZZ), S1);  // S2 - S1
     const fq29 PP = fq29::sqr(P);
     if (PP.maybe_zero8()) {
       if (P.to_fq().is_zero()) {
@@ -361,8 +350,7 @@ struct g1_acc29 {
     ZZ = fq29::mul(fq29::mul(ZZ, o.ZZ), PP);
     ZZZ = fq29::mul(fq29::mul(ZZZ, o.ZZZ), PPP);
     const fq29 Qv = fq29::mul(U1, PP);
-    const fq29 R2 = fq29::sqr(R);
-    X = fq29::sub<16, 3>(R2, fq29::add(PPP, fq29::add(Qv, Qv))).norm();
+    X = fq29::carry_sub<16, 3>(fq29::sqr_cols(R), fq29::add(PPP, fq29::add(Qv, Qv)));
     const fq29 T = fq29::sub<64, 1>(Qv, X);
     Y = fq29::mul2(R, T, S1, fq29::neg<3, 1>(PPP));  // R*T - S1*PPP
   }

@@ -402,8 +402,17 @@ __device__ __forceinline__ void combine_enqueue(uint32_t* list, uint32_t* cnt, u
 __device__ __forceinline__ uint32_t* run_rec(uint32_t* raw, uint64_t i) { return raw + RAW29_WORDS * i; }
 __device__ __forceinline__ const uint32_t* run_rec(const uint32_t* raw, uint64_t i) { return raw + RAW29_WORDS * i; }
 
+// Blocks of 256 per CU in the bucket accumulation (= waves per SIMD). 3 fits the 166-VGPR add loop
+// and is 2.5 % faster for one MSM alone; 2 leaves a third of every register file to the kernels of
+// the other proofs in flight and of the second MSM lane: +0.7 % proofs/s and 15.6 -> 14.8 ms
+// single-proof latency (same-box A/B, 128-proof runs).
 #ifndef KGS_ACC_WAVES
-#define KGS_ACC_WAVES 3
+#define KGS_ACC_WAVES 2
+#endif
+// diagnostic builds only (wrong results): KGS_DIAG_GATHER_MASK confines the point gathers to a small,
+// cache-resident part of the table, to measure what the random HBM gathers cost the add loop
+#ifndef KGS_DIAG_GATHER_MASK
+#define KGS_DIAG_GATHER_MASK 0x7fffffffu
 #endif
 __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __restrict__ segowner,
                                                     uint32_t* __restrict__ chunklist, uint32_t* __restrict__ chunkcnt,
@@ -434,7 +443,7 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
   // entry e is added (the gathers' latency hides behind ~11 K cycles of VALU work)
   uint32_t v = sorted[start];
   uint32_t vn = start + 1 < end ? sorted[start + 1] : 0u;
-  const uint4* pt = reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(v & 0x7fffffffu));
+  const uint4* pt = reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(v & KGS_DIAG_GATHER_MASK));
   uint4 a0 = pt[0], a1 = pt[1], a2 = pt[2], a3 = pt[3];
   for (uint32_t e = (uint32_t)start; e < end32; e++) {
     if (e >= bend32) {
@@ -447,7 +456,7 @@ __global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __r
     const uint32_t yw[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
     const bool negy = (v & 0x80000000u) != 0;
     if (e + 1 < end32) {
-      const uint4* pn = reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(vn & 0x7fffffffu));
+      const uint4* pn = reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(vn & KGS_DIAG_GATHER_MASK));
       a0 = pn[0]; a1 = pn[1]; a2 = pn[2]; a3 = pn[3];
       v = vn;
       if (e + 2 < end32) vn = sorted[e + 2];

@@ -9,7 +9,6 @@ import math
 import os
 import re
 
-import pytest
 
 Q = 21888242871839275222246405745257275088696311157297823662689037894645226208583
 MASK = (1 << 29) - 1
@@ -94,6 +93,21 @@ def _mul2(a, b, c, d):  # fq29::mul2: (a*b + c*d) / 2^261, one reduction
     return V(out, MASK)
 
 
+def _fused(cols_bound):
+    """carry_sub folds a product's carry pass into a difference: its columns are read as int64"""
+    assert cols_bound < (1 << 63), "signed column overflow %.3f" % math.log2(cols_bound)
+
+
+def _mul_cols(a, b):
+    _fused(9 * a.limb * b.limb + 9 * MASK * MASK + (1 << 36))
+    return _mul(a, b)
+
+
+def _sqr_cols(a):
+    _fused(10 * a.limb * a.limb + 9 * MASK * MASK + (1 << 36))
+    return _sqr(a)
+
+
 def _add(a, b):
     return V(a.val + b.val, a.limb + b.limb)
 
@@ -114,27 +128,22 @@ def _norm(a):
     return V(a.val, MASK)
 
 
-def madd_bound(vb, legacy=False):
-    """g1_acc29::add_aff step by step (same k, s as the header); returns the output bound.
-    legacy=True models the -DKGS_NO_SQR29 build (plain products, Y3 from two reduced products)."""
-    sqr = (lambda a: _mul(a, a)) if legacy else _sqr
+def madd_bound(vb):
+    """g1_acc29::add_aff step by step (same k, s as the header); returns the output bound"""
     X1 = Y1 = ZZ1 = ZZZ1 = V(vb, MASK)
     x2 = y2 = V(Q, MASK)
-    U2, S2 = _mul(x2, ZZ1), _mul(y2, ZZZ1)
-    P = _norm(_sub(U2, X1, 30, 1))
+    U2, S2 = _mul_cols(x2, ZZ1), _mul(y2, ZZZ1)
+    P = _norm(_sub(U2, X1, 30, 1))            # carry_sub<30, 1>
     Rb = _neg(Y1, 32, 2)                      # K - Y1, then +- S2
     for j in range(9):                        # the negated branch: K_j - Y1_j - S2_j >= 0
         assert _spread(32, 2)[j] >= Y1.limb_max(j) + S2.limb_max(j)
     R = _norm(V(Rb.val + S2.val, Rb.limb + S2.limb))
-    PP = sqr(P)
+    PP = _sqr(P)
     assert PP.val <= 8 * Q                    # maybe_zero8's candidate set covers PP
-    PPP, Qv, R2 = _mul(P, PP), _mul(X1, PP), sqr(R)
+    PPP, Qv, R2 = _mul(P, PP), _mul(X1, PP), _sqr_cols(R)
     nX = _norm(_sub(R2, _add(PPP, _add(Qv, Qv)), 16, 3))
     T = _sub(Qv, nX, 64, 1)
-    if legacy:
-        Y3 = _norm(_sub(_mul(R, T), _mul(Y1, PPP), 16, 1))
-    else:
-        Y3 = _mul2(R, T, Y1, _neg(PPP, 3, 1))  # R*T + Y1*(3q - PPP)
+    Y3 = _mul2(R, T, Y1, _neg(PPP, 3, 1))     # R*T + Y1*(3q - PPP)
     ZZ3, ZZZ3 = _mul(ZZ1, PP), _mul(ZZZ1, PPP)
     # the raw-record conversion (to_fq) and the rare-path checks multiply by C256 < q
     for c in (P, R, nX, Y3, ZZ3, ZZZ3):
@@ -145,7 +154,7 @@ def madd_bound(vb, legacy=False):
 def add_bound(vb):
     """g1_acc29::add (accumulator + accumulator, the combine / bit-sum trees) step by step"""
     X1 = Y1 = ZZ1 = ZZZ1 = X2 = Y2 = ZZ2 = ZZZ2 = V(vb, MASK)
-    U1, U2, S1, S2 = _mul(X1, ZZ2), _mul(X2, ZZ1), _mul(Y1, ZZZ2), _mul(Y2, ZZZ1)
+    U1, U2, S1, S2 = _mul(X1, ZZ2), _mul_cols(X2, ZZ1), _mul(Y1, ZZZ2), _mul_cols(Y2, ZZZ1)
     P = _norm(_sub(U2, U1, 8, 1))
     R = _norm(_sub(S2, S1, 8, 1))
     PP = _sqr(P)
@@ -154,7 +163,7 @@ def add_bound(vb):
     ZZ3 = _mul(_mul(ZZ1, ZZ2), PP)
     ZZZ3 = _mul(_mul(ZZZ1, ZZZ2), PPP)
     Qv = _mul(U1, PP)
-    R2 = _sqr(R)
+    R2 = _sqr_cols(R)
     nX = _norm(_sub(R2, _add(PPP, _add(Qv, Qv)), 16, 3))
     T = _sub(Qv, nX, 64, 1)
     Y3 = _mul2(R, T, S1, _neg(PPP, 3, 1))
@@ -176,24 +185,22 @@ def test_full_add_bounds():
     assert 2 * Q <= vb
 
 
-@pytest.mark.parametrize("legacy", [False, True])
-def test_add_aff_bounds_fixed_point(legacy):
+def test_add_aff_bounds_fixed_point():
     # initial accumulator: a table point (< q) with ZZ = ZZZ = 2^261 mod q; negated y: 2q - y
     vb = 2 * Q
     for _ in range(50):
-        nxt = max(madd_bound(vb, legacy), vb)
+        nxt = max(madd_bound(vb), vb)
         if nxt == vb:
             break
         vb = nxt
-    assert madd_bound(vb, legacy) <= vb
+    assert madd_bound(vb) <= vb
     assert math.log2(vb) < 258.6  # field29.hpp: coordinates < 2^258.6
 
 
 def test_spread_constants_used_by_header():
     t = _hdr()
     uses = set(re.findall(r"(?:sub|neg)<(\d+), (\d+)>", t))
-    assert uses == {("30", "1"), ("32", "2"), ("16", "3"), ("64", "1"), ("16", "1"), ("2", "1"), ("3", "1"),
-                    ("8", "1")}
+    assert uses == {("30", "1"), ("32", "2"), ("16", "3"), ("64", "1"), ("2", "1"), ("3", "1"), ("8", "1")}
     for k, s in uses:
         _spread(int(k), int(s))
     # the initial negation 2q - y of a canonical y (< q) stays nonnegative per limb
