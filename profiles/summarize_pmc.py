@@ -8,6 +8,7 @@ per lane, one record per lane), i.e. a different pattern, so both the raw and th
 figures are recorded and the RAW one is used as `traffic` (it already exceeds the algorithmic
 bytes ~1.9x: each 64 B record pulls a 128 B line).
 usage: summarize_pmc.py <pmc_FETCH_SIZE dir> <pmc_WRITE_SIZE dir> <round tag>
+(both passes over `python3 profiles/msm_loop.py 20 3`)
 """
 import collections
 import csv
@@ -37,8 +38,8 @@ def main():
                         "fetch_bytes_raw": round(fa), "fetch_bytes_x2": round(2 * fa), "write_bytes": round(wa)})
     with open(os.path.join(HERE, f"pmc_{tag}.json"), "w") as fh:
         json.dump({"round": tag, "kernels": kernels}, fh, indent=1)
-    # bench MSM leg: 2^20 points, c = 16 -> 2^24 entries / L = 64 -> 262144 segments (grid threads)
-    acc = [k for k in kernels if k["kernel"].endswith("k_accumulate") and k["grid_threads"] == 262144]
+    # run on profiles/msm_loop.py (every MSM is a 2^20-point one): the k_accumulate dispatches
+    acc = [k for k in kernels if k["kernel"].endswith("k_accumulate")]
     if acc:
         a = acc[0]
         with open(os.path.join(HERE, "pmc_accumulate.json"), "w") as fh:
