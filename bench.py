@@ -21,9 +21,9 @@ Extra fields in the JSON line:
   host_buffer_boundary : PCIe-inclusive latency of kgs_prove on pageable host buffers (the drop-in path)
   latency_ms_single_proof / round_ms_single_proof : one proof at a time on one context (2 MSM lanes)
   msm       : live HIP-event timing of the MSM phases at N = n (points/s, G1 adds/s)
-  roofline  : the dominant kernel (MSM bucket accumulation, k_accumulate) against the chip's
-              v_mad_u64_u32 issue rate (INT-VALU bound); traffic = PMC FETCH+WRITE
-              from profiles/
+  roofline  : the dominant kernel (MSM bucket accumulation, k_accumulate) in algorithmic Fq products/s
+              against the chip's mad-only product rate (INT-VALU bound); traffic =
+              PMC FETCH+WRITE from profiles/
   hbm_view  : proof-level bytes (SURVEY.md §8d's count over the reference op list) per second vs 8 TB/s
   extra_configs : BASELINE.json configs[2] (grand-product at n), configs[3] (grand-sum n = 2^24) and
               configs[4] (selected-vector k = 4, n = 2^22) — single GPU at N = 1, every MSM
@@ -402,6 +402,8 @@ def main():
             traffic = None
     roofline = {"bound": "valu", "kernel": "k_accumulate", "achieved": round(achieved, 2), "peak": round(peak, 2),
                 "unit": "G Fq-products/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                "bound_note": "integer-VALU issue bound (254-bit Montgomery products on v_mad_u64_u32): neither the "
+                              "HBM roof (the kernel moves ~1 TB/s of 8) nor MFMA (no dense contraction) applies",
                 "mad_issue_frac": round(entries.value * MADS_PER_ADD / (acc_ms / 1e3) / MAD_PEAK, 4),
                 "g1_adds_per_s": round(entries.value / (acc_ms / 1e3)),
                 "algorithmic_bytes_per_launch": 68 * entries.value,
@@ -437,7 +439,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32x8 (BN254 Fr/Fq Montgomery, int VALU)",
+        "dtype": "u32 limbs (BN254 Fr/Fq Montgomery: 8 x 32-bit; MSM buckets 9 x 29-bit), int VALU",
         "data": "synthetic (PCG64-seeded multisets, T = rot(F); synthetic ptau, tau = keccak('kgs-bench-tau'))",
         "config": {"workload": f"{args.kind} prover, n=2^{nbits}, k={args.npols}, no selectors, inputs resident in HBM",
                    "nbits": nbits, "npols": args.npols, "selectors": False, "parallelism": f"replicas x{world}", "inflight_per_gpu": args.inflight,

@@ -57,7 +57,10 @@ def test_to_mont(ctx9):
     assert ctx9.fr_to_mont(common.std_bytes(v)) == common.mont_bytes(v)
 
 
-@pytest.mark.parametrize("logm", list(range(0, 13)))
+# 0..10: radix-8/4/2 passes only; 11..17: LDS-staged passes of 6/5/4 stages (k_ntt_lds_pass<3,3>,
+# <3,2>, <2,2>) followed by radix-8/4/2 passes, in every combination (11 = 6+5, 13 = 6+6+1,
+# 14 = 6+6+2, 15 = 6+6+3, 16 = 6+6+4, 17 = 6+6+5)
+@pytest.mark.parametrize("logm", list(range(0, 18)))
 def test_ntt(ctx9, logm):
     rnd = random.Random(logm)
     v = rv(rnd, 1 << logm)
