@@ -113,12 +113,13 @@ struct kgs_ctx {
 
   ~kgs_ctx() {
     hipSetDevice(device);
+    // every stream may still read pool buffers or pinned staging: drain all before freeing
     if (st) hipStreamSynchronize(st);
+    if (st2) hipStreamSynchronize(st2);
+    if (st_copy) hipStreamSynchronize(st_copy);
     for (auto& kv : pool) hipFree(kv.second.p);
     if (h_pin) hipHostFree(h_pin);
     if (h_io) hipHostFree(h_io);
-    if (st2) hipStreamSynchronize(st2);
-    if (st_copy) hipStreamSynchronize(st_copy);
     if (ev_fork) hipEventDestroy(ev_fork);
     if (ev_copy) hipEventDestroy(ev_copy);
     if (st_copy) hipStreamDestroy(st_copy);
