@@ -23,6 +23,7 @@ static inline unsigned nb(uint64_t work, unsigned bs = 256) { return (unsigned)(
 // ------------------------------------------------------------------ window table precompute
 __global__ void __launch_bounds__(256) k_tab_dbl(uint32_t* __restrict__ tmp, const uint32_t* __restrict__ prev,
                                                  uint64_t npts, int c) {
+  KGS_AUX_PRIO();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= npts) return;
   g1_aff a = g1_aff::load(prev + 16 * i);
@@ -35,6 +36,7 @@ __global__ void __launch_bounds__(256) k_tab_dbl(uint32_t* __restrict__ tmp, con
 template <int CH>
 __global__ void __launch_bounds__(256) k_batch_affine(uint32_t* __restrict__ out, const uint32_t* __restrict__ in,
                                                       uint32_t* __restrict__ scratch, uint64_t npts) {
+  KGS_AUX_PRIO();
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t start = t * CH;
   if (start >= npts) return;
@@ -65,6 +67,7 @@ __global__ void __launch_bounds__(256) k_batch_affine(uint32_t* __restrict__ out
 
 // table coordinates x*2^256 -> x*2^261 (the fq29 Montgomery form of the bucket accumulation)
 __global__ void __launch_bounds__(256) k_tab_to29(uint32_t* __restrict__ table, uint64_t nelem) {
+  KGS_AUX_PRIO();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nelem) return;
   fq c;
@@ -153,6 +156,7 @@ constexpr int SORT_SPT = KGS_SORT_SPT;  // scalars per thread in the histogram /
 template <int C>
 __global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ bh, const uint32_t* __restrict__ sc,
                                                    uint64_t N, int lob, int NH, uint32_t nblk) {
+  KGS_AUX_PRIO();
   // per-block partition histogram, stored transposed: bh[p * nblk + block]
   constexpr int W = (255 + C - 1) / C;
   __shared__ uint32_t h[256];
@@ -176,6 +180,7 @@ __global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ bh, co
 // grid = NH workgroups: exclusive scan of one partition's per-block counts (in place) and its total
 __global__ void __launch_bounds__(256) k_sort_scan_blocks(uint32_t* __restrict__ bh, uint32_t* __restrict__ ptot,
                                                           uint32_t nblk) {
+  KGS_AUX_PRIO();
   __shared__ uint32_t part[256];
   uint32_t* row = bh + (uint64_t)blockIdx.x * nblk;
   const uint32_t per = (nblk + 255) / 256;
@@ -202,6 +207,7 @@ __global__ void __launch_bounds__(256) k_sort_scan_blocks(uint32_t* __restrict__
 // hi_off[p] = exclusive scan of partition totals (NH <= 256); offsets[B+1] = total
 __global__ void __launch_bounds__(64) k_sort_scan(uint32_t* __restrict__ hi_off, const uint32_t* __restrict__ ptot,
                                                   int NH, uint32_t* __restrict__ offsets, uint32_t B) {
+  KGS_AUX_PRIO();
   const uint32_t total = wave_excl_scan256(ptot, hi_off, NH);
   if (threadIdx.x == 0) {
     hi_off[NH] = total;
@@ -216,6 +222,7 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
                                                    const uint32_t* __restrict__ bh, const uint32_t* __restrict__ ptot,
                                                    const uint32_t* __restrict__ hi_off, const uint32_t* __restrict__ sc,
                                                    uint64_t N, uint64_t Nsrs, int lob, int NH, uint32_t nblk) {
+  KGS_AUX_PRIO();
   constexpr int W = (255 + C - 1) / C;
   extern __shared__ uint32_t smem[];
   uint32_t* sval = smem;                                        // 256 * SORT_SPT * W
@@ -284,6 +291,7 @@ __device__ __forceinline__ void chunk_range(uint32_t s0, uint32_t s1, int g, uin
 // grid (SL_G, NH): locnt[(p * nb + lo) * SL_G + g] = #entries of chunk g of partition p with this lo
 __global__ void __launch_bounds__(SL_THREADS) k_lo_count(uint32_t* __restrict__ locnt, const uint8_t* __restrict__ tlo,
                                                          const uint32_t* __restrict__ hi_off, int lob) {
+  KGS_AUX_PRIO();
   __shared__ uint32_t cnt[256];
   const int g = blockIdx.x, p = blockIdx.y;
   const int nb = 1 << lob;
@@ -299,6 +307,7 @@ __global__ void __launch_bounds__(SL_THREADS) k_lo_count(uint32_t* __restrict__ 
 // grid NH, 256 threads: bases (in place over locnt) and the bucket offsets of keys (p << lob) + lo + 1
 __global__ void __launch_bounds__(256) k_lo_scan(uint32_t* __restrict__ locnt, uint32_t* __restrict__ offsets,
                                                  const uint32_t* __restrict__ hi_off, int lob) {
+  KGS_AUX_PRIO();
   __shared__ uint32_t tot[256], pre[256];
   const int p = blockIdx.x;
   const int nb = 1 << lob;
@@ -328,6 +337,7 @@ __global__ void __launch_bounds__(SL_THREADS) k_lo_scatter(uint32_t* __restrict_
                                                            const uint32_t* __restrict__ tval,
                                                            const uint8_t* __restrict__ tlo,
                                                            const uint32_t* __restrict__ hi_off, int lob) {
+  KGS_AUX_PRIO();
   __shared__ uint32_t cur[256], tcnt[256], toff[256];
   __shared__ uint32_t sv[SL_TILE];
   __shared__ uint8_t sl[SL_TILE];
@@ -498,6 +508,7 @@ __global__ void __launch_bounds__(256) k_combine_level(uint32_t* __restrict__ ra
                                                        const uint32_t* __restrict__ cnt_in,
                                                        uint32_t* __restrict__ list_out, uint32_t* __restrict__ cnt_out,
                                                        uint32_t L, uint64_t stride) {
+  KGS_AUX_PRIO();
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= *cnt_in) return;
   const uint64_t s = list_in[t];
@@ -515,6 +526,7 @@ __global__ void __launch_bounds__(256) k_combine_level(uint32_t* __restrict__ ra
 __global__ void __launch_bounds__(256) k_combine(uint32_t* __restrict__ raw, uint32_t nbins,
                                                  const uint32_t* __restrict__ offsets, uint32_t B, uint32_t L,
                                                  uint64_t stride) {
+  KGS_AUX_PRIO();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t b = (g >> 1) + 1;  // buckets 1..B
   const uint32_t sub = g & 1;
@@ -556,6 +568,7 @@ __device__ __forceinline__ g1_acc29 block_tree_sum(g1_acc29 v, uint32_t* lds) {
 }
 
 __global__ void __launch_bounds__(256) k_rowcol(uint32_t* __restrict__ rc, const uint32_t* __restrict__ raw, int c) {
+  KGS_AUX_PRIO();
   __shared__ __attribute__((aligned(16))) uint32_t lds[128 * RAW29_WORDS];
   const int l = c / 2, h = c - 1 - l;  // l = ceil((c-1)/2)
   const uint32_t r = blockIdx.x, t = threadIdx.x;
@@ -575,6 +588,7 @@ __global__ void __launch_bounds__(256) k_rowcol(uint32_t* __restrict__ rc, const
 // k - l set (l <= k < c-1), or S_B (k = c-1); 256-bit XYZZ out for the host
 __global__ void __launch_bounds__(128) k_bitsum_rc(uint32_t* __restrict__ T, const uint32_t* __restrict__ rc,
                                                    const uint32_t* __restrict__ raw, int c) {
+  KGS_AUX_PRIO();
   __shared__ __attribute__((aligned(16))) uint32_t lds[64 * RAW29_WORDS];
   const int l = c / 2, h = c - 1 - l;
   const int k = blockIdx.x;
@@ -675,6 +689,7 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
 // out[i] = s_i * G with s_i = from_mont(sc[i]); tbl[j*256 + d] = (d * 2^(8j)) G, affine.
 __global__ void __launch_bounds__(256) k_fixed_base(uint32_t* __restrict__ out_xyzz, const uint32_t* __restrict__ sc,
                                                     uint64_t count, const uint32_t* __restrict__ tbl) {
+  KGS_AUX_PRIO();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   fr s = fr::load(sc + 8 * i).from_mont();

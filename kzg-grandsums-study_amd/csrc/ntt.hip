@@ -29,6 +29,7 @@ __global__ void __launch_bounds__(256) k_ntt_dif_pass(uint32_t* __restrict__ dat
                                                       const uint32_t* __restrict__ pre,
                                                       const uint32_t* __restrict__ tw, int logM, int logm,
                                                       int s0) {
+  KGS_AUX_PRIO();
   const uint64_t m = 1ull << logm;
   const uint64_t ngroups = m >> K;
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -83,6 +84,7 @@ __global__ void __launch_bounds__(256) k_ntt_dit_pass(uint32_t* __restrict__ dat
                                                       const uint32_t* __restrict__ tw, int logM, int logm,
                                                       int s0, const uint32_t* __restrict__ post,
                                                       const uint32_t* __restrict__ post_s) {
+  KGS_AUX_PRIO();
   const uint64_t m = 1ull << logm;
   const uint64_t ngroups = m >> K;
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -203,6 +205,7 @@ __global__ void __launch_bounds__(256) k_ntt_lds_pass(uint32_t* __restrict__ dat
                                                       const uint32_t* __restrict__ tw, int logm, int s0,
                                                       const uint32_t* __restrict__ post,
                                                       const uint32_t* __restrict__ post_s) {
+  KGS_AUX_PRIO();
   constexpr int K = K1 + K2;
   constexpr int LBLOG = 11 - K;
   constexpr int LB = 1 << LBLOG;
@@ -363,6 +366,7 @@ void ntt_dit(hipStream_t st, uint32_t* out, const uint32_t* in, int in_bitrev, i
 // tw[j] = w^j for j < count, computed in chunks of 64 from w^(64 t) by square-and-multiply.
 __global__ void k_powers(uint32_t* __restrict__ out, uint64_t count, const uint32_t* __restrict__ wp,
                          const uint32_t* __restrict__ scale) {
+  KGS_AUX_PRIO();
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t start = t * 64;
   if (start >= count) return;
@@ -390,6 +394,7 @@ void launch_powers(hipStream_t st, uint32_t* out, uint64_t count, const uint32_t
 
 __global__ void k_scale_copy(uint32_t* __restrict__ out, const uint32_t* __restrict__ in, uint64_t n,
                              const uint32_t* __restrict__ tab, const uint32_t* __restrict__ sc) {
+  KGS_AUX_PRIO();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   fr x = fr::load(in + 8 * i);
@@ -404,6 +409,7 @@ void launch_scale_copy(hipStream_t st, uint32_t* out, const uint32_t* in, uint64
 }
 
 __global__ void k_bitrev_copy(uint32_t* __restrict__ out, const uint32_t* __restrict__ in, int logm) {
+  KGS_AUX_PRIO();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (1ull << logm)) return;
   uint64_t j = logm ? bitrev((uint32_t)i, logm) : 0;

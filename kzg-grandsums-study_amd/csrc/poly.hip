@@ -21,6 +21,7 @@ __device__ __forceinline__ uint32_t brev(uint32_t x, int bits) {
 
 // ---------------------------------------------------------------------------- conversions
 __global__ void k_to_mont(uint32_t* __restrict__ out, const uint32_t* __restrict__ in, uint64_t n) {
+  KGS_AUX_PRIO();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   fr::load(in + 8 * i).to_mont().store(out + 8 * i);
@@ -31,6 +32,7 @@ void launch_to_mont(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t 
 
 // ---------------------------------------------------------------------------- linear combination
 __global__ void k_lincomb(uint32_t* __restrict__ out, uint64_t n, LinComb lc) {
+  KGS_AUX_PRIO();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   fr acc = fr::zero();
@@ -120,6 +122,7 @@ template <bool PROD, bool SEL>
 __global__ void __launch_bounds__(256) k_builder_tileprod(uint32_t* __restrict__ tileprod, const uint32_t* f,
                                                           const uint32_t* t, const uint32_t* sf, const uint32_t* st_,
                                                           const uint32_t* gp, uint64_t n) {
+  KGS_AUX_PRIO();
   __shared__ uint32_t lds[256 * 8];
   const fr g = fr::load(gp);
   const uint64_t base = (uint64_t)blockIdx.x * BT_TILE + threadIdx.x * BT_PER;
@@ -139,6 +142,7 @@ __global__ void __launch_bounds__(256) k_builder_tileprod(uint32_t* __restrict__
 // Single block: inverse of every tile product via prefix/suffix products and ONE inversion.
 __global__ void __launch_bounds__(1024) k_tile_inverse(uint32_t* __restrict__ tinv, const uint32_t* __restrict__ tp,
                                                        uint32_t ntiles) {
+  KGS_AUX_PRIO();
   __shared__ uint32_t lds[1024 * 8];
   __shared__ uint32_t tot[8];
   const uint32_t t = threadIdx.x;
@@ -200,6 +204,7 @@ __global__ void __launch_bounds__(256) k_builder_finish(uint32_t* __restrict__ o
                                                         const uint32_t* __restrict__ tinv, const uint32_t* f,
                                                         const uint32_t* t, const uint32_t* sf, const uint32_t* st_,
                                                         const uint32_t* gp, uint64_t n) {
+  KGS_AUX_PRIO();
   __shared__ uint32_t lds[256 * 8];
   const fr g = fr::load(gp);
   const uint64_t base = (uint64_t)blockIdx.x * BT_TILE + threadIdx.x * BT_PER;
@@ -282,6 +287,7 @@ __global__ void __launch_bounds__(256) k_builder_finish(uint32_t* __restrict__ o
 // Single block: exclusive scan of tile accumulators -> carry per tile (in place).
 template <bool PROD>
 __global__ void __launch_bounds__(1024) k_tile_carry(uint32_t* __restrict__ acc, uint32_t ntiles) {
+  KGS_AUX_PRIO();
   __shared__ uint32_t lds[1024 * 8];
   const uint32_t t = threadIdx.x;
   const uint32_t per = (ntiles + 1023) / 1024;
@@ -309,6 +315,7 @@ __global__ void __launch_bounds__(1024) k_tile_carry(uint32_t* __restrict__ acc,
 template <bool PROD>
 __global__ void k_apply_carry(uint32_t* __restrict__ out, const uint32_t* __restrict__ carry, uint64_t n,
                               uint32_t* __restrict__ flag) {
+  KGS_AUX_PRIO();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t tile = i / BT_TILE;
@@ -354,6 +361,7 @@ __global__ void __launch_bounds__(256) k_quotient(uint32_t* __restrict__ q, cons
                                                   const uint32_t* __restrict__ SF, const uint32_t* __restrict__ ST,
                                                   const uint32_t* __restrict__ inv_nxm1, const uint32_t* __restrict__ sc,
                                                   int lcs, uint32_t rot) {
+  KGS_AUX_PRIO();
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t cs = 1ull << lcs;
   if (p >= cs) return;
@@ -415,6 +423,7 @@ template <bool PROD, bool SEL>
 __global__ void k_divcheck(uint32_t* __restrict__ flag, const uint32_t* __restrict__ S, const uint32_t* __restrict__ f,
                            const uint32_t* __restrict__ t, const uint32_t* __restrict__ sfp, const uint32_t* __restrict__ stp,
                            const uint32_t* __restrict__ sc, uint64_t n) {
+  KGS_AUX_PRIO();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const fr alpha = fr::load(sc), gamma = fr::load(sc + 8);
@@ -462,6 +471,7 @@ void launch_divcheck(hipStream_t st, bool prod, bool sel, uint32_t* flag, const 
 // xp[l] = x^(8 * 2^l), l = 0..7 ; x itself at xp[8]
 __global__ void __launch_bounds__(256) k_eval_tiles(uint32_t* __restrict__ part, EvalBatch eb,
                                                     const uint32_t* __restrict__ xp, uint32_t ntiles_max) {
+  KGS_AUX_PRIO();
   __shared__ uint32_t lds[256 * 8];
   const int pi = blockIdx.y;
   const uint32_t* c = eb.src[pi];
@@ -495,6 +505,7 @@ void launch_eval_tiles(hipStream_t st, uint32_t* part, const EvalBatch& eb, cons
 // tile carries: carry[b] = r_{start of tile b+1}, from tile Horner values h_b (part) with Z = z^2048.
 __global__ void __launch_bounds__(1024) k_div_carries(uint32_t* __restrict__ carry, const uint32_t* __restrict__ h,
                                                       uint32_t ntiles, const uint32_t* __restrict__ zT) {
+  KGS_AUX_PRIO();
   __shared__ uint32_t lds[1024 * 8];
   const uint32_t t = threadIdx.x;
   const uint32_t per = (ntiles + 1023) / 1024;
@@ -532,6 +543,7 @@ __global__ void __launch_bounds__(1024) k_div_carries(uint32_t* __restrict__ car
 __global__ void __launch_bounds__(256) k_div_finish(uint32_t* __restrict__ q, uint32_t* __restrict__ flag,
                                                     const uint32_t* __restrict__ a, uint64_t L,
                                                     const uint32_t* __restrict__ carry, const uint32_t* __restrict__ xp) {
+  KGS_AUX_PRIO();
   __shared__ uint32_t lds[256 * 8];
   const fr z = fr::load(xp + 8 * 8);
   const uint64_t base = (uint64_t)blockIdx.x * BT_TILE + threadIdx.x * BT_PER;
@@ -583,6 +595,7 @@ void launch_divide(hipStream_t st, uint32_t* q, uint32_t* flag, const uint32_t* 
 // ---------------------------------------------------------------------------- Fr batch inverse
 // out[i] = in[i]^-1 (0 -> 0), per-thread Montgomery trick over CH elements (domain setup only).
 __global__ void k_fr_batch_inv(uint32_t* __restrict__ out, const uint32_t* __restrict__ in, uint64_t n, uint32_t ch) {
+  KGS_AUX_PRIO();
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t start = t * ch;
   if (start >= n) return;
@@ -611,6 +624,7 @@ void launch_fr_batch_inv(hipStream_t st, uint32_t* out, const uint32_t* in, uint
 // tw holds w_M^j for j < M/2; w_M^(j + M/2) = -w_M^j.
 __global__ void k_nxm1(uint32_t* __restrict__ out, const uint32_t* __restrict__ tw, uint64_t halfM,
                        const uint32_t* __restrict__ gp, const uint32_t* __restrict__ np, int lcs, uint64_t wstride) {
+  KGS_AUX_PRIO();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (1ull << lcs)) return;
   uint64_t e = i * wstride;
