@@ -63,6 +63,12 @@ def synth_evals(n, idx):
 
 
 BENCH_TAU = None
+
+
+def log(msg):
+    """progress on stderr (stdout carries only the JSON line)"""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 # v_mad_u64_u32 issue rate of the whole chip: 256 CUs x 4 SIMDs x 64 lanes / 4.97 cycles x 2.4 GHz
 # (measured: profiles/ubench/issue_rates.hip). One bucket add (madd-2008-s in 9 x 29-bit limbs,
 # field29.hpp) issues 1,467 of them: 6 products x 162, 2 squares x 126 (45 symmetric partial
@@ -118,6 +124,7 @@ def large_leg(K, torch, dist, rank, world, local, nb, k, selected, proofs, label
     (kgs_ctx_set_shard over torch.distributed = RCCL). The last proof is checked with the native
     verifier (kgs_verify_ptau: transcript replay + pairing)."""
     n = 1 << nb
+    log(f"large leg: {label}")
     ctx = K.Context(local)
     t0 = time.time()
     ptau, _ = shared_ptau(ctx, nb, dist)
@@ -215,6 +222,7 @@ def main():
     nbits = args.nbits
     n = 1 << nbits
     kind = K.GRANDSUM if args.kind == "grandsum" else K.GRANDPRODUCT
+    log("writing / loading the ptau")
     ptau, t_gen = shared_ptau(ctx, nbits, dist)
     t0 = time.time()
     ctx.load_ptau(ptau, nbits)
@@ -260,6 +268,7 @@ def main():
     # single-proof latency below uses context 0 with two lanes (kgs_ctx_set_msm_lanes)
     for c in ctxs:
         c.set_msm_lanes(1 if len(ctxs) > 1 else 2)
+    log("warm-up")
     steps(max(args.warmup, len(ctxs)))
     # single-proof latency (one proof at a time on one context), outside the timed region
     ctx.set_msm_lanes(2)
@@ -281,6 +290,7 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    log("timed region")
     ts = time.perf_counter()
     steps(args.steps)
     torch.cuda.synchronize()
@@ -294,6 +304,7 @@ def main():
 
     # ---------------- host-buffer boundary (what the JS / Python drop-in modules call): kgs_prove on
     # pageable host buffers, including the H2D copy of F/T and the D2H Montgomery write-back
+    log(f"timed: {value:.2f} proofs/s; host-buffer and JS legs")
     host_leg = None
     if rank == 0:
         hf = [synth_evals(n, 1000 * rank + i)[0].tobytes() for i in range(args.npols)]
@@ -313,13 +324,17 @@ def main():
         js_dir = os.path.join(HERE, "kzg-grandsums-study_amd", "js")
         if shutil.which("node") and os.path.exists(os.path.join(js_dir, "build", "kgs_addon.node")):
             try:
-                out = subprocess.run(["node", os.path.join(js_dir, "test", "time_prove.js"), ptau, str(nbits), "5"],
-                                     capture_output=True, text=True, timeout=300)
+                # latency: best of 4 one-at-a-time proofs; throughput: 8 concurrent chains of 3
+                # awaited prover() calls over the module's context pool (4 contexts per GPU)
+                env = dict(os.environ, KGS_JS_CONTEXTS=str(args.inflight), KGS_DEVICES=str(local))
+                out = subprocess.run(["node", os.path.join(js_dir, "test", "time_prove.js"), ptau, str(nbits), "3",
+                                      str(2 * args.inflight)], capture_output=True, text=True, timeout=300, env=env)
                 host_leg["javascript_module"] = json.loads(out.stdout.strip().splitlines()[-1])
             except Exception as e:  # the JS leg must not hide the GPU number
                 host_leg["javascript_module"] = {"error": str(e)[:200]}
 
     # ---------------- extra configs (BASELINE.json configs[2] and [4]), outside the timed region
+    log("extra configs")
     extra_cfg = {}
     if args.extra_legs:
         # C3: grand-product at the same n, same contexts / inputs (replicas per GPU)
@@ -334,9 +349,15 @@ def main():
         steps(gp_steps)
         torch.cuda.synchronize()
         el = max_over_ranks(time.perf_counter() - t1)
+        # one proof of this leg checked with the native verifier (transcript replay + pairing)
+        d_f0, d_t0 = bufs[0]
+        coms1, evs1 = ctxs[0].prove_device(kind, nbits, d_f0, d_t0)
+        cn1, en1 = K.proof_names(kind, args.npols, False)
+        vf1 = K.grandsum_verifier if kind == K.GRANDSUM else K.grandproduct_verifier
         extra_cfg["grandproduct_vs_grandsum" if kind_main == K.GRANDSUM else "grandsum_vs_grandproduct"] = {
             "workload": f"{'grandproduct' if kind == K.GRANDPRODUCT else 'grandsum'} prover, n=2^{nbits}, k={args.npols}, no selectors",
-            "proofs_per_s": round(gp_steps * world / el, 4), "proofs": gp_steps * world}
+            "proofs_per_s": round(gp_steps * world / el, 4), "proofs": gp_steps * world,
+            "proof_verified": vf1(ptau, {"commitments": dict(zip(cn1, coms1)), "evaluations": dict(zip(en1, evs1))}, nbits)}
         kind = kind_main
         # C5 (N = 1: one GPU; N > 1: every MSM point-range sharded over all ranks, RCCL all-gather)
         for c in ctxs[1:]:
@@ -354,6 +375,7 @@ def main():
             dist.destroy_process_group()
         return
 
+    log("MSM leg")
     # ---------------- MSM leg: live HIP-event timing of the phases at N = n
     sc = torch.from_numpy(synth_evals(n, 777)[0].reshape(-1).copy()).to(f"cuda:{local}")
     phase = (ctypes.c_double * 4)()
@@ -419,6 +441,7 @@ def main():
                 "note": "the proof is INT-VALU bound (MSM bucket accumulation), not HBM bound"}
 
     # ---------------- CPU baseline (oracle/c port of the reference op list), N = 1 only
+    log("CPU baseline")
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         try:

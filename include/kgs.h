@@ -14,8 +14,11 @@
  *  - Every call returns 0 on success or a negative KGS_E_* code; kgs_last_error() returns the
  *    message of the last failure on the calling thread. Semantic failures reproduce the
  *    reference's Error messages verbatim.
- *  - A context owns one HIP device, one stream, the device-resident SRS (+ MSM window tables) and
- *    the NTT domain tables. Contexts are not re-entrant.
+ *  - A context owns one HIP device, its HIP streams and work buffers. Every entry point taking a
+ *    context holds that context's mutex for the whole call: calls on one context from several
+ *    threads are serialised (a busy context blocks, it is never entered twice); independent
+ *    contexts run concurrently. The SRS window tables and the NTT domain tables are read-only and
+ *    shared by all contexts of a device (one copy per device, refcounted).
  */
 #ifndef KGS_H
 #define KGS_H
@@ -45,7 +48,10 @@ typedef struct kgs_ctx kgs_ctx_t;
 const char* kgs_last_error(void);
 const char* kgs_version(void);
 
-/* Create / destroy a context on HIP device `device`. */
+/* Number of visible HIP devices (the JS backend spreads its context pool over them). */
+int kgs_device_count(int* count);
+/* Create / destroy a context on HIP device `device`. kgs_ctx_destroy waits for a call still
+ * running on the context. */
 int kgs_ctx_create(int device, kgs_ctx_t** out);
 void kgs_ctx_destroy(kgs_ctx_t* ctx);
 
@@ -77,9 +83,14 @@ int kgs_ctx_set_msm_lanes(kgs_ctx_t* ctx, int lanes);
 /* Load a .ptau file (binfileutils layout, sections 1-3) and make the first 2^(nbits_max+1) G1
  * points device-resident, together with the MSM window tables and the NTT tables for domains
  * up to 2^nbits_max (nbits_max < 0: the file's power). Replaces readBinFile + readPTauHeader +
- * fd.readToBuffer(section 2) (src/grandsum/mset_eq_kzg_prover.js:15-16,83-85; src/ptau_utils.js:3-24).
- * Re-loading the same (path, nbits_max) is a no-op (device SRS cache). */
+ * fd.readToBuffer(section 2) (src/grandsum/mset_eq_kzg_prover.js:15-16,83-85; src/ptau_utils.js:3-24),
+ * which reads exactly domainSize*2 points per call: pass the proof's nBits as nbits_max.
+ * Device SRS cache, grow-only: a context that already holds tables of the same file (same resolved
+ * path, size and mtime) for a domain >= 2^nbits_max keeps them (no-op); tables of that file built
+ * for a large enough domain by another context on the device are shared, not rebuilt. */
 int kgs_srs_load_ptau(kgs_ctx_t* ctx, const char* path, int nbits_max);
+/* Power of a ptau file from its header only (readPTauHeader, src/ptau_utils.js:3-24). */
+int kgs_ptau_power(const char* path, int* power);
 /* Same from in-memory LEM points (npts >= 2). `power` is the ceremony power to report. */
 int kgs_srs_load_points(kgs_ctx_t* ctx, const uint8_t* g1_lem, uint64_t npts, int power, int nbits_max);
 /* power of the loaded ptau, number of resident points, MSM window c */

@@ -50,6 +50,8 @@ def lib():
         L.kgs_ctx_destroy.argtypes = [ctypes.c_void_p]
         L.kgs_ctx_destroy.restype = None
         L.kgs_srs_load_ptau.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
+        L.kgs_ptau_power.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
+        L.kgs_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.kgs_srs_load_points.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
         L.kgs_srs_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint64),
                                    ctypes.POINTER(ctypes.c_int)]
@@ -136,6 +138,19 @@ def keccak256(data: bytes) -> bytes:
     src = ctypes.create_string_buffer(bytes(data), max(1, len(data)))
     _check(lib().kgs_keccak256(src, len(data), out))
     return out.raw
+
+
+def ptau_power(path):
+    """Power of a ptau file, from its header only (kgs_ptau_power; readPTauHeader, ptau_utils.js:3-24)."""
+    p = ctypes.c_int()
+    _check(lib().kgs_ptau_power(os.fsencode(path), ctypes.byref(p)))
+    return p.value
+
+
+def device_count():
+    n = ctypes.c_int()
+    _check(lib().kgs_device_count(ctypes.byref(n)))
+    return n.value
 
 
 def shard_range(n, rank, world):
@@ -405,6 +420,7 @@ def _context(device=0):
 def _prover(kind, pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, device=0):
     """src/grandsum/mset_eq_kzg_prover.js:12-142 — input checks with the reference's messages, then
     the HIP prover. Overwrites evalsFs[i].eval / evalsTs[i].eval with Montgomery form (:147-148)."""
+    power = ptau_power(pTauFilename)  # the header is read first (prover.js:15-16)
     if not isinstance(evalsFs, (list, tuple)):
         evalsFs = [evalsFs]
     if not isinstance(evalsTs, (list, tuple)):
@@ -432,11 +448,11 @@ def _prover(kind, pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None
     nbits = (n0 - 1).bit_length() if n0 > 0 else 0
     if n0 != (1 << nbits):
         raise ValueError("Polynomial length must be a power of two.")
-    ctx = _context(device)
-    ctx.load_ptau(pTauFilename)
-    power, _, _ = ctx.srs_info()
     if power < nbits:
         raise ValueError("The Powers of Tau file is not sufficiently large to commit the polynomials.")
+    ctx = _context(device)
+    # only the 2^(nbits+1) points this proof commits with (prover.js:83-85); grow-only device cache
+    ctx.load_ptau(pTauFilename, nbits)
     coms, evs, mf, mt = ctx.prove(kind, nbits, [e.eval for e in evalsFs], [e.eval for e in evalsTs],
                                   evalsSelF.eval if is_selected else None,
                                   evalsSelT.eval if is_selected else None)

@@ -18,7 +18,10 @@
 #include <stdlib.h>
 #include <string.h>
 #include <chrono>
+#include <algorithm>
 #include <map>
+#include <mutex>
+#include <sys/stat.h>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -60,6 +63,22 @@ static void check_launch() {
 
 using host::fr_w;
 
+// Every device allocation goes through here. KGS_DEBUG_ALLOC_LIMIT=<bytes> (fault injection for the
+// tests) makes any single request above that size fail as out-of-memory.
+hipError_t dev_malloc(void** p, size_t bytes) {
+  if (const char* e = getenv("KGS_DEBUG_ALLOC_LIMIT")) {
+    const unsigned long long lim = strtoull(e, nullptr, 10);
+    if (lim && bytes > lim) {
+      *p = nullptr;
+      return hipErrorOutOfMemory;
+    }
+  }
+  return hipMalloc(p, bytes);
+}
+
+// multisets per proof (the reference has no limit; this only bounds host-side bookkeeping)
+constexpr int KGS_MAX_POLS = 1024;
+
 #ifndef KGS_C_MAX
 #define KGS_C_MAX 17
 #endif
@@ -69,10 +88,46 @@ struct DBuf {
   size_t bytes = 0;
 };
 
+// Read-only device tables shared by every context on a device (one copy per device, not per
+// in-flight context): the SRS window tables of a ptau (keyed by file identity and the domain they
+// were loaded for) and the NTT / coset twiddle tables (the largest domain built so far serves every
+// smaller one: stage tables tw[h + t] = w_2h^t do not depend on the maximum domain). Published only
+// after their build has completed (stream synchronised), released when the last context drops them.
+struct SrsTables {
+  int device = 0;
+  std::string file;  // file identity (path + size + mtime) or "mem#<id>"
+  int power = -1, nbits_max = -1;
+  MsmTables tb;
+  ~SrsTables() {
+    if (tb.table) {
+      hipSetDevice(device);
+      hipFree(tb.table);
+    }
+  }
+};
+
+struct DomainTables {
+  int device = 0, logM = -1;
+  uint32_t* mem = nullptr;
+  uint32_t *tw_fwd = nullptr, *tw_inv = nullptr, *coset_pow = nullptr, *coset_ipow = nullptr, *invm = nullptr;
+  ~DomainTables() {
+    if (mem) {
+      hipSetDevice(device);
+      hipFree(mem);
+    }
+  }
+};
+
+std::mutex g_reg_mu;  // lock order: kgs_ctx::mu, then g_reg_mu
+std::vector<std::weak_ptr<SrsTables>> g_srs_reg;
+std::vector<std::weak_ptr<DomainTables>> g_dom_reg;
 
 }  // namespace
 
 struct kgs_ctx {
+  // every C-ABI entry point that touches the context holds mu: a busy context blocks its caller,
+  // it is never entered twice (the JS backend runs prove() calls on libuv worker threads)
+  std::mutex mu;
   int device = 0;
   hipStream_t st = nullptr;
   std::map<std::string, DBuf> pool;
@@ -86,12 +141,14 @@ struct kgs_ctx {
   uint32_t* d_scal = nullptr;  // device scalar area
   size_t d_scal_off = 0;
   static constexpr size_t SCAL_BYTES = 1 << 16;
-  // SRS
-  std::string srs_key;
+  // SRS (shared, read-only) and this context's views of it
+  std::shared_ptr<SrsTables> srs;
   int srs_power = -1;
   int nbits_max = -1;
   MsmTables tb;
   MsmWork mw;
+  uint64_t work_npts = 0;  // MSM work buffers (both lanes) are sized for this many points
+  int msm_slots = 0;       // commitments in flight per proof (msm_T slots)
   // second MSM lane: independent commitments of one round (R1's F_i/T_i, R5's two W) alternate
   // between st and st2 (own work buffers), so one MSM's latency-bound tail overlaps the other's
   // bucket accumulation
@@ -101,7 +158,8 @@ struct kgs_ctx {
   MsmWork mw2;
   int msm_lanes = 2;  // kgs_ctx_set_msm_lanes
   uint64_t msm_nseg_max = 0;
-  // domain tables (M = 2^logM)
+  // domain tables (M = 2^logM; shared) and this context's views of them
+  std::shared_ptr<DomainTables> dom;
   int logM = -1;
   uint32_t *tw_fwd = nullptr, *tw_inv = nullptr, *coset_pow = nullptr, *coset_ipow = nullptr, *invm = nullptr;
   std::map<std::pair<int, int>, uint32_t*> nxm1;  // (nbits, lcs) -> 1/(n(x-1)) on the coset (bitrev)
@@ -125,18 +183,26 @@ struct kgs_ctx {
     if (st_copy) hipStreamDestroy(st_copy);
     if (st2) hipStreamDestroy(st2);
     if (st) hipStreamDestroy(st);
+    {
+      std::lock_guard<std::mutex> lk(g_reg_mu);  // shared tables are released under the registry lock
+      srs.reset();
+      dom.reset();
+    }
   }
 
+  // A failed (re)allocation leaves the slot empty (bytes = 0), never a stale size over a freed block.
   uint32_t* buf(const std::string& name, size_t bytes) {
     DBuf& b = pool[name];
     if (b.bytes < bytes) {
       if (b.p) {
-        HC(hipStreamSynchronize(st));
+        sync();  // any stream may still use the old block
         HC(hipFree(b.p));
         b.p = nullptr;
+        b.bytes = 0;
       }
-      HC(hipMalloc(&b.p, bytes < 64 ? 64 : bytes));
-      b.bytes = bytes < 64 ? 64 : bytes;
+      const size_t sz = bytes < 64 ? 64 : bytes;
+      HC(dev_malloc(&b.p, sz));
+      b.bytes = sz;
     }
     return (uint32_t*)b.p;
   }
@@ -146,6 +212,7 @@ struct kgs_ctx {
         sync();
         HC(hipHostFree(h_io));
         h_io = nullptr;
+        h_io_bytes = 0;
       }
       HC(hipHostMalloc((void**)&h_io, bytes, hipHostMallocDefault));
       h_io_bytes = bytes;
@@ -155,8 +222,11 @@ struct kgs_ctx {
   void ensure_pin(size_t bytes) {
     if (h_pin_bytes >= bytes) return;
     if (h_pin) {
-      HC(hipStreamSynchronize(st));
+      sync();
       HC(hipHostFree(h_pin));
+      h_pin = nullptr;
+      h_pin_bytes = 0;
+      h_pin_off = 0;
     }
     HC(hipHostMalloc((void**)&h_pin, bytes, hipHostMallocDefault));
     h_pin_bytes = bytes;
@@ -190,20 +260,50 @@ struct kgs_ctx {
     h_pin_off = 0;
     d_scal_off = 0;
   }
+  void use_srs(const std::shared_ptr<SrsTables>& s) {
+    srs = s;
+    tb = s ? s->tb : MsmTables{};
+    srs_power = s ? s->power : -1;
+    nbits_max = s ? s->nbits_max : -1;
+  }
+  void use_domain(const std::shared_ptr<DomainTables>& d) {
+    dom = d;
+    logM = d->logM;
+    tw_fwd = d->tw_fwd;
+    tw_inv = d->tw_inv;
+    coset_pow = d->coset_pow;
+    coset_ipow = d->coset_ipow;
+    invm = d->invm;
+  }
 };
 
 namespace {
 
 // ------------------------------------------------------------------ domain tables
+// Shared per device: a context asking for 2^logM reuses any published table of at least that size.
 void ensure_domain(kgs_ctx& c, int logM) {
   if (c.logM >= logM) return;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  for (auto& w : g_dom_reg) {
+    auto d = w.lock();
+    if (d && d->device == c.device && d->logM >= logM) {
+      c.use_domain(d);
+      c.nxm1.clear();
+      return;
+    }
+  }
   const uint64_t M = 1ull << logM;
-  // stage twiddle tables: tw[h + t] = w_{2h}^t for h = 2^l, l < logM (entries 1..M-1)
-  c.tw_fwd = c.buf("tw_fwd", 32 * M);
-  c.tw_inv = c.buf("tw_inv", 32 * M);
-  c.coset_pow = c.buf("coset_pow", 32 * M);
-  c.coset_ipow = c.buf("coset_ipow", 32 * M);
-  c.invm = c.buf("invm", 32 * (logM + 1));
+  auto d = std::make_shared<DomainTables>();
+  d->device = c.device;
+  // stage twiddle tables: tw[h + t] = w_{2h}^t for h = 2^l, l < logM (entries 1..M-1); coset powers
+  // g^i, g^-i (g = 5); 1/2^l for l <= logM
+  const size_t words = (size_t)8 * (4 * M + logM + 1);
+  HC(dev_malloc((void**)&d->mem, 4 * words));
+  d->tw_fwd = d->mem;
+  d->tw_inv = d->tw_fwd + 8 * M;
+  d->coset_pow = d->tw_inv + 8 * M;
+  d->coset_ipow = d->coset_pow + 8 * M;
+  d->invm = d->coset_ipow + 8 * M;
   c.reset_staging();
   std::vector<Fr> consts;
   for (int l = 0; l < logM; l++) {
@@ -214,23 +314,27 @@ void ensure_domain(kgs_ctx& c, int logM) {
   Fr g = Fr::from_u64(5);
   consts.push_back(g);
   consts.push_back(g.inverse());
-  uint32_t* d = c.scal(consts.data(), (int)consts.size());
+  uint32_t* dc = c.scal(consts.data(), (int)consts.size());
   for (int l = 0; l < logM; l++) {
     const uint64_t h = 1ull << l;
-    launch_powers(c.st, c.tw_fwd + 8 * h, h, d + 16 * l, nullptr);
-    launch_powers(c.st, c.tw_inv + 8 * h, h, d + 16 * l + 8, nullptr);
+    launch_powers(c.st, d->tw_fwd + 8 * h, h, dc + 16 * l, nullptr);
+    launch_powers(c.st, d->tw_inv + 8 * h, h, dc + 16 * l + 8, nullptr);
   }
-  launch_powers(c.st, c.coset_pow, M, d + 16 * logM, nullptr);
-  launch_powers(c.st, c.coset_ipow, M, d + 16 * logM + 8, nullptr);
+  launch_powers(c.st, d->coset_pow, M, dc + 16 * logM, nullptr);
+  launch_powers(c.st, d->coset_ipow, M, dc + 16 * logM + 8, nullptr);
   std::vector<Fr> im(logM + 1);
   for (int l = 0; l <= logM; l++) im[l] = Fr::from_u64(1ull << l).inverse();
   uint8_t* h = c.pin(32 * (logM + 1));
   for (int l = 0; l <= logM; l++) im[l].to_bytes(h + 32 * l);
-  HC(hipMemcpyAsync(c.invm, h, 32 * (logM + 1), hipMemcpyHostToDevice, c.st));
+  HC(hipMemcpyAsync(d->invm, h, 32 * (logM + 1), hipMemcpyHostToDevice, c.st));
   check_launch();
-  c.reset_staging();
+  c.reset_staging();  // built: publish
+  d->logM = logM;
+  g_dom_reg.erase(std::remove_if(g_dom_reg.begin(), g_dom_reg.end(), [](auto& w) { return w.expired(); }),
+                  g_dom_reg.end());
+  g_dom_reg.push_back(d);
+  c.use_domain(d);
   c.nxm1.clear();
-  c.logM = logM;
 }
 
 uint32_t* get_nxm1(kgs_ctx& c, int nbits, int lcs) {
@@ -279,21 +383,12 @@ int choose_c(uint64_t npts) {
   return cc;
 }
 
-void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int nbits_max, const std::string& key) {
-  if (npts < 2) throw KgsError(KGS_E_ARG, "SRS needs at least 2 points");
-  c.sync();
-  const int cc = choose_c(npts);
-  const int W = (255 + cc - 1) / cc;
-  c.tb.npts = npts;
-  c.tb.c = cc;
-  c.tb.W = W;
-  c.tb.table = c.buf("msm_table", (size_t)W * npts * 64);
-  HC(hipMemcpy(c.tb.table, lem, npts * 64, hipMemcpyHostToDevice));
-  uint32_t* tmp = c.buf("msm_tmp_xyzz", npts * 128);
-  uint32_t* scr = c.buf("msm_tmp_scr", npts * 32);
-  msm_build_table(c.st, c.tb.table, npts, cc, W, tmp, scr);
-  check_launch();
-  // work buffers for N <= npts
+// MSM work buffers of both lanes, for MSMs of up to npts points with window c
+void ensure_msm_work(kgs_ctx& c) {
+  const uint64_t npts = c.tb.npts;
+  if (c.work_npts >= npts && c.work_npts) return;
+  c.work_npts = 0;  // invalid until every buffer below exists
+  const int cc = c.tb.c, W = c.tb.W;
   const uint64_t E = npts * W;
   const uint32_t B = 1u << (cc - 1);
   uint64_t nseg = (1ull << 18) + (1ull << 16) + 2;
@@ -316,11 +411,75 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
     w.raw29 = c.buf("msm_raw29" + sfx, 160 * ((size_t)B + 2 + nseg));
     w.part = c.buf("msm_part" + sfx, 160 * (size_t)(2 << (cc / 2)));  // row + column sums
   }
-  c.srs_power = power;
-  c.nbits_max = nbits_max;
-  ensure_domain(c, nbits_max + 1);
+  c.work_npts = npts;
+}
+
+// Build (or share) the window tables of `npts` LEM points. `file` identifies the source; an empty
+// `file` (in-memory points) is never shared. The context's SRS is replaced only once the new tables
+// and the work buffers exist: a failed load leaves the context without an SRS ("no SRS loaded"),
+// never with a half-built one.
+void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int nbits_max, const std::string& file) {
+  if (npts < 2) throw KgsError(KGS_E_ARG, "SRS needs at least 2 points");
   c.sync();
-  c.srs_key = key;
+  c.use_srs(nullptr);
+  c.work_npts = 0;
+  std::shared_ptr<SrsTables> s;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    if (!file.empty())
+      for (auto& w : g_srs_reg) {
+        auto t = w.lock();
+        if (t && t->device == c.device && t->file == file && t->nbits_max >= nbits_max) {
+          s = t;
+          break;
+        }
+      }
+    if (!s) {
+      int cc = choose_c(npts);
+      int W = (255 + cc - 1) / cc;
+      // sorted entries pack j * npts + i into 31 bits (bit 31 = sign): widen the window until it fits
+      while ((uint64_t)W * npts > (1ull << 31) && cc < KGS_C_MAX) W = (255 + (++cc) - 1) / cc;
+      if ((uint64_t)W * npts > (1ull << 31)) throw KgsError(KGS_E_SRS, "SRS too large for the MSM entry index");
+      auto t = std::make_shared<SrsTables>();
+      t->device = c.device;
+      t->file = file;
+      t->power = power;
+      t->nbits_max = nbits_max;
+      t->tb.npts = npts;
+      t->tb.c = cc;
+      t->tb.W = W;
+      HC(dev_malloc((void**)&t->tb.table, (size_t)W * npts * 64));
+      HC(hipMemcpy(t->tb.table, lem, npts * 64, hipMemcpyHostToDevice));
+      // build temporaries are released right after the build (they would otherwise stay in the pool)
+      struct Tmp {
+        void* p = nullptr;
+        ~Tmp() {
+          if (p) hipFree(p);
+        }
+      } tmp, scr;
+      HC(dev_malloc(&tmp.p, npts * 128));
+      HC(dev_malloc(&scr.p, npts * 32));
+      msm_build_table(c.st, t->tb.table, npts, cc, W, (uint32_t*)tmp.p, (uint32_t*)scr.p);
+      check_launch();
+      HC(hipStreamSynchronize(c.st));
+      g_srs_reg.erase(std::remove_if(g_srs_reg.begin(), g_srs_reg.end(), [](auto& w) { return w.expired(); }),
+                      g_srs_reg.end());
+      if (!file.empty()) g_srs_reg.push_back(t);
+      s = t;
+    }
+  }
+  ensure_domain(c, s->nbits_max + 1);
+  MsmTables keep = c.tb;
+  c.tb = s->tb;  // ensure_msm_work sizes from the new tables
+  try {
+    ensure_msm_work(c);
+  } catch (...) {
+    c.tb = keep;
+    c.use_srs(nullptr);
+    throw;
+  }
+  c.sync();
+  c.use_srs(s);
 }
 
 // ------------------------------------------------------------------ MSM (commit)
@@ -352,9 +511,10 @@ Commit commit_launch(kgs_ctx& c, const uint32_t* scalars, uint64_t N, int slot, 
   Commit cm;
   cm.N = N;
   const int cc = c.tb.c;
-  uint32_t* dT = c.buf("msm_T", (size_t)64 * cc * 128) + (size_t)slot * cc * 32;
+  const int slots = c.msm_slots > 64 ? c.msm_slots : 64;
+  if (slot >= slots) throw KgsError(KGS_E_ARG, "too many commitments in flight");
   if (N > c.tb.npts) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
-  if (slot >= 64) throw KgsError(KGS_E_ARG, "too many commitments in flight");
+  uint32_t* dT = c.buf("msm_T", (size_t)slots * cc * 128) + (size_t)slot * cc * 32;
   cm.h_T = c.pin((size_t)cc * 128);
   uint64_t lo = 0, hi = N;
   if (c.shard_world > 1) shard_range(N, c.shard_rank, c.shard_world, lo, hi);
@@ -439,18 +599,21 @@ EvalJob eval_launch(kgs_ctx& c, const std::vector<const uint32_t*>& src, const s
   uint64_t maxlen = 1;
   for (auto l : len) maxlen = l > maxlen ? l : maxlen;
   j.ntiles = (uint32_t)((maxlen + EVAL_TILE - 1) / EVAL_TILE);
-  EvalBatch eb;
-  eb.npolys = (int)src.size();
-  if (eb.npolys > EB_MAX) throw KgsError(KGS_E_ARG, "too many polynomials in one evaluation batch");
-  for (int i = 0; i < eb.npolys; i++) {
-    eb.src[i] = src[i];
-    eb.len[i] = len[i];
-  }
+  const int np = (int)src.size();
   uint32_t* xp = xpowers(c, x);
-  size_t bytes = (size_t)32 * j.ntiles * eb.npolys;
+  size_t bytes = (size_t)32 * j.ntiles * (np ? np : 1);
   uint32_t* dpart = c.buf("eval_part_" + std::to_string(slot), bytes);
-  launch_eval_tiles(c.st, dpart, eb, xp, j.ntiles);
-  check_launch();
+  // batches of EB_MAX polynomials per launch (any number of multisets), partials contiguous per poly
+  for (int p0 = 0; p0 < np; p0 += EB_MAX) {
+    EvalBatch eb;
+    eb.npolys = np - p0 < EB_MAX ? np - p0 : EB_MAX;
+    for (int i = 0; i < eb.npolys; i++) {
+      eb.src[i] = src[p0 + i];
+      eb.len[i] = len[p0 + i];
+    }
+    launch_eval_tiles(c.st, dpart + (size_t)8 * j.ntiles * p0, eb, xp, j.ntiles);
+    check_launch();
+  }
   j.h_part = c.pin(bytes);
   HC(hipMemcpyAsync(j.h_part, dpart, bytes, hipMemcpyDeviceToHost, c.st));
   return j;
@@ -477,12 +640,43 @@ struct ProveIn {
   std::function<void()> after_round1;             // called once round 1 is synchronised
 };
 
-void set_lc_term(LinComb& lc, const uint32_t* src, uint64_t len, const Fr& coef) {
-  if (lc.nterms >= LC_MAX) throw KgsError(KGS_E_ARG, "too many linear-combination terms");
-  lc.src[lc.nterms] = src;
-  lc.len[lc.nterms] = len;
-  coef.to_bytes((uint8_t*)lc.coef[lc.nterms]);
-  lc.nterms++;
+// out[i] = sum_k coef_k * src_k[i] (zero beyond len_k) + (i == 0 ? c0 : 0), any number of terms:
+// launches of LC_MAX terms, every launch after the first adds the previous partial (out itself,
+// element-wise in place) as its first term
+struct LcTerms {
+  std::vector<const uint32_t*> src;
+  std::vector<uint64_t> len;
+  std::vector<Fr> coef;
+  Fr c0 = Fr::zero();
+  void add(const uint32_t* s, uint64_t l, const Fr& k) {
+    src.push_back(s);
+    len.push_back(l);
+    coef.push_back(k);
+  }
+};
+
+void run_lincomb(hipStream_t st, uint32_t* out, uint64_t n, const LcTerms& t) {
+  size_t k = 0;
+  bool first = true;
+  do {
+    LinComb lc{};
+    if (!first) {
+      lc.src[0] = out;
+      lc.len[0] = n;
+      Fr::one().to_bytes((uint8_t*)lc.coef[0]);
+      lc.nterms = 1;
+    }
+    for (; k < t.src.size() && lc.nterms < LC_MAX; k++) {
+      lc.src[lc.nterms] = t.src[k];
+      lc.len[lc.nterms] = t.len[k];
+      t.coef[k].to_bytes((uint8_t*)lc.coef[lc.nterms]);
+      lc.nterms++;
+    }
+    (first ? t.c0 : Fr::zero()).to_bytes((uint8_t*)lc.c0);
+    launch_lincomb(st, out, n, lc);
+    check_launch();
+    first = false;
+  } while (k < t.src.size());
 }
 
 void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out) {
@@ -506,7 +700,18 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     throw KgsError(KGS_E_SRS, "The Powers of Tau file is not sufficiently large to commit the polynomials.");
   if (nbits > c.nbits_max) throw KgsError(KGS_E_SRS, "SRS loaded for a smaller maximum domain; reload with larger nbits_max");
   if (k < 1) throw KgsError(KGS_E_ARG, "The number of multisets must be greater than 0.");
-  if (k > 10) throw KgsError(KGS_E_ARG, "at most 10 multisets per proof are supported");
+  if (k > KGS_MAX_POLS) throw KgsError(KGS_E_ARG, "too many multisets");
+  // pinned staging for this proof's host round trips: commit partials (c x 128 B each), the
+  // round-4 Horner tile partials (32 B per 2048 coefficients per evaluated polynomial), flags and
+  // scalars (each bump allocation rounds up to 64 B)
+  const int ncom_all = 2 * k + (in.sel_f ? 2 : 0) + 4;
+  c.msm_slots = ncom_all + 4;
+  {
+    const size_t ntl = (size_t)((n + EVAL_TILE - 1) / EVAL_TILE);
+    const size_t need = (size_t)(ncom_all + 4) * ((size_t)c.tb.c * 128 + 64) + 32 * ntl * (2 * k + 3) + 64 * 8 +
+                        ((size_t)kgs_ctx::SCAL_BYTES * 2) + (1 << 20);
+    c.ensure_pin(need > ((size_t)8 << 20) ? need : ((size_t)8 << 20));
+  }
   c.reset_staging();
   uint32_t* flags = c.buf("flags", 64);
   HC(hipMemsetAsync(flags, 0, 64, c.st));
@@ -589,17 +794,17 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     uint32_t* b_te = c.buf("tcomb", E);
     uint32_t* b_F = c.buf("polF", E);
     uint32_t* b_T = c.buf("polT", E);
-    LinComb l1{}, l2{}, l3{}, l4{};
+    LcTerms l1, l2, l3, l4;
     for (int i = 0; i < k; i++) {
-      set_lc_term(l1, fm[i], n, bpow[i]);
-      set_lc_term(l2, tm[i], n, bpow[i]);
-      set_lc_term(l3, Fc[i], n, bpow[i]);
-      set_lc_term(l4, Tc[i], n, bpow[i]);
+      l1.add(fm[i], n, bpow[i]);
+      l2.add(tm[i], n, bpow[i]);
+      l3.add(Fc[i], n, bpow[i]);
+      l4.add(Tc[i], n, bpow[i]);
     }
-    launch_lincomb(c.st, b_fe, n, l1);
-    launch_lincomb(c.st, b_te, n, l2);
-    launch_lincomb(c.st, b_F, n, l3);
-    launch_lincomb(c.st, b_T, n, l4);
+    run_lincomb(c.st, b_fe, n, l1);
+    run_lincomb(c.st, b_te, n, l2);
+    run_lincomb(c.st, b_F, n, l3);
+    run_lincomb(c.st, b_T, n, l4);
     fcomb = b_fe;
     tcomb = b_te;
     polF = b_F;
@@ -741,7 +946,7 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   const Fr one = Fr::one();
   Fr selBin = Fr::zero();  // alpha^3 selTBin + alpha^2 selFBin
   if (sel) selBin = ((sTx - sTx.sqr()) * alpha + (sFx - sFx.sqr())) * alpha * alpha;
-  LinComb lw{};
+  LcTerms lw;
   Fr c0;
   uint32_t* Pbuf;
   uint64_t L;
@@ -752,53 +957,53 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     const Fr fg = fxi + gamma, tg = txi + gamma;
     Fr rc = sxiw * fg * tg + (sel ? sTx * fg - sFx * tg : fxi - txi);
     c0 = selBin + alpha * rc;
-    set_lc_term(lw, Sc, n, l1 - alpha * fg * tg);
-    set_lc_term(lw, Qc, qlen, zh.neg());
+    lw.add(Sc, n, l1 - alpha * fg * tg);
+    lw.add(Qc, qlen, zh.neg());
     for (int i = 0; i < k; i++) {
-      set_lc_term(lw, Fc[i], n, vp[1 + i]);
+      lw.add(Fc[i], n, vp[1 + i]);
       c0 = c0 - vp[1 + i] * fx[i];
     }
     for (int i = 0; i < k; i++) {
-      set_lc_term(lw, Tc[i], n, vp[1 + k + i]);
+      lw.add(Tc[i], n, vp[1 + k + i]);
       c0 = c0 - vp[1 + k + i] * tx[i];
     }
     if (sel) {
-      set_lc_term(lw, sFc, n, vp[2 * k + 1]);
-      set_lc_term(lw, sTc, n, vp[2 * k + 2]);
+      lw.add(sFc, n, vp[2 * k + 1]);
+      lw.add(sTc, n, vp[2 * k + 2]);
       c0 = c0 - vp[2 * k + 1] * sFx - vp[2 * k + 2] * sTx;
     }
   } else {
     const Fr fg = fxi + gamma;
     const Fr dF = sel ? sFx * (fg - one) + one : fg;
     c0 = selBin + alpha * sxiw * (sel ? sTx * (gamma - one) + one : gamma) - l1;
-    set_lc_term(lw, polT, n, alpha * sxiw * (sel ? sTx : one));
-    set_lc_term(lw, Sc, n, l1 - alpha * dF);
-    set_lc_term(lw, Qc, qlen, zh.neg());
+    lw.add(polT, n, alpha * sxiw * (sel ? sTx : one));
+    lw.add(Sc, n, l1 - alpha * dF);
+    lw.add(Qc, qlen, zh.neg());
     for (int i = 0; i < k; i++) {
-      set_lc_term(lw, Fc[i], n, vp[1 + i]);
+      lw.add(Fc[i], n, vp[1 + i]);
       c0 = c0 - vp[1 + i] * fx[i];
     }
     if (sel) {
-      set_lc_term(lw, sFc, n, vp[k + 1]);
-      set_lc_term(lw, sTc, n, vp[k + 2]);
+      lw.add(sFc, n, vp[k + 1]);
+      lw.add(sTc, n, vp[k + 2]);
       c0 = c0 - vp[k + 1] * sFx - vp[k + 2] * sTx;
     }
   }
-  c0.to_bytes((uint8_t*)lw.c0);
+  lw.c0 = c0;
   L = qlen > n ? qlen : n;
   Pbuf = c.buf("Pw", 32 * L);
   uint32_t* Wx = c.buf("Wxi", 32 * L);
-  launch_lincomb(c.st, Pbuf, L, lw);
+  run_lincomb(c.st, Pbuf, L, lw);
   const uint32_t dtiles = (uint32_t)((L + EVAL_TILE - 1) / EVAL_TILE);
   launch_divide(c.st, Wx, flags + 2, Pbuf, L, xpowers(c, xi), c.buf("div_part", 32 * (dtiles + 1)),
                 c.buf("div_carry", 32 * (dtiles + 1)));
   // W_{xi w} = (S - S(xi w)) / (X - xi w)
-  LinComb l2{};
-  set_lc_term(l2, Sc, n, one);
-  sxiw.neg().to_bytes((uint8_t*)l2.c0);
+  LcTerms l2;
+  l2.add(Sc, n, one);
+  l2.c0 = sxiw.neg();
   uint32_t* P2 = c.buf("Pw2", E);
   uint32_t* Wxw = c.buf("Wxiw", E);
-  launch_lincomb(c.st, P2, n, l2);
+  run_lincomb(c.st, P2, n, l2);
   launch_divide(c.st, Wxw, flags + 3, P2, n, xpowers(c, xiw), c.buf("div_part2", 32 * (ntiles + 1)),
                 c.buf("div_carry2", 32 * (ntiles + 1)));
   check_launch();
@@ -930,8 +1135,13 @@ int kgs_ctx_create(int device, kgs_ctx_t** out) {
   }
 }
 
-void kgs_ctx_destroy(kgs_ctx_t* ctx) { delete ctx; }
+void kgs_ctx_destroy(kgs_ctx_t* ctx) {
+  if (!ctx) return;
+  { std::lock_guard<std::mutex> lk(ctx->mu); }  // wait for a call still running on another thread
+  delete ctx;
+}
 
+#define CTX_LOCK(c) std::lock_guard<std::mutex> ctx_lock_(c->mu)
 #define API_BEGIN try {
 #define API_END                               \
   }                                           \
@@ -944,41 +1154,73 @@ void kgs_ctx_destroy(kgs_ctx_t* ctx) { delete ctx; }
   }                                           \
   return KGS_OK;
 
+int kgs_device_count(int* count) {
+  API_BEGIN
+  if (!count) throw KgsError(KGS_E_ARG, "NULL argument");
+  int n = 0;
+  HC(hipGetDeviceCount(&n));
+  *count = n;
+  API_END
+}
+
 int kgs_srs_load_points(kgs_ctx_t* ctx, const uint8_t* g1_lem, uint64_t npts, int power, int nbits_max) {
   API_BEGIN
   if (!ctx || !g1_lem) throw KgsError(KGS_E_ARG, "NULL argument");
+  CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
   if (nbits_max < 0) nbits_max = power;
+  if (nbits_max > 28) throw KgsError(KGS_E_ARG, "nbits_max must be <= 28");
   uint64_t need = 1ull << (nbits_max + 1);
   if (npts < need) need = npts;
-  load_points(*ctx, g1_lem, need, power, nbits_max, "mem");
+  load_points(*ctx, g1_lem, need, power, nbits_max, "");
+  API_END
+}
+
+int kgs_ptau_power(const char* path, int* power) {
+  API_BEGIN
+  if (!path || !power) throw KgsError(KGS_E_ARG, "NULL argument");
+  FILE* f = fopen(path, "rb");
+  if (!f) throw KgsError(KGS_E_IO, std::string("cannot open ") + path);
+  std::unique_ptr<FILE, int (*)(FILE*)> guard(f, fclose);
+  *power = read_ptau_header(f, path).power;
   API_END
 }
 
 int kgs_srs_load_ptau(kgs_ctx_t* ctx, const char* path, int nbits_max) {
   API_BEGIN
   if (!ctx || !path) throw KgsError(KGS_E_ARG, "NULL argument");
+  CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
   FILE* f = fopen(path, "rb");
   if (!f) throw KgsError(KGS_E_IO, std::string("cannot open ") + path);
   std::unique_ptr<FILE, int (*)(FILE*)> guard(f, fclose);
   PtauInfo info = read_ptau_header(f, path);
   if (nbits_max < 0 || nbits_max > info.power) nbits_max = info.power;
-  std::string key = std::string(path) + "#" + std::to_string(nbits_max);
-  if (ctx->srs_key == key) return KGS_OK;
+  if (nbits_max > 28) throw KgsError(KGS_E_SRS, "ptau power above 28 is not supported");
+  // file identity: the reference re-reads the file on every call, so a rewritten file (same path,
+  // new size or mtime) must not hit the device cache
+  struct stat stt;
+  if (fstat(fileno(f), &stt) != 0) throw KgsError(KGS_E_IO, std::string("cannot stat ") + path);
+  char real[4096];
+  const char* rp = realpath(path, real) ? real : path;
+  const std::string file = std::string(rp) + "#" + std::to_string((long long)stt.st_size) + "#" +
+                           std::to_string((long long)stt.st_mtim.tv_sec) + "." + std::to_string((long long)stt.st_mtim.tv_nsec);
+  // grow-only: tables loaded for a larger domain of the same file serve every smaller proof
+  if (ctx->srs && ctx->srs->file == file && ctx->srs->nbits_max >= nbits_max) return KGS_OK;
   uint64_t avail = info.s2_size / 64;
   uint64_t need = 1ull << (nbits_max + 1);
   if (need > avail) need = avail;
   std::vector<uint8_t> pts(need * 64);
   if (fseeko(f, (off_t)info.s2_pos, SEEK_SET) || fread(pts.data(), 1, pts.size(), f) != pts.size())
     throw KgsError(KGS_E_IO, "cannot read tauG1 section");
-  load_points(*ctx, pts.data(), need, info.power, nbits_max, key);
+  load_points(*ctx, pts.data(), need, info.power, nbits_max, file);
   API_END
 }
 
 int kgs_srs_info(kgs_ctx_t* ctx, int* power, uint64_t* npts, int* window_c) {
   API_BEGIN
   if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  CTX_LOCK(ctx);
   if (power) *power = ctx->srs_power;
   if (npts) *npts = ctx->tb.npts;
   if (window_c) *window_c = ctx->tb.c;
@@ -1007,6 +1249,7 @@ int kgs_ptau_write_synthetic(kgs_ctx_t* ctx, const char* path, int power, const 
   std::vector<uint8_t> g1(n1 * 64);
   std::vector<uint8_t> tbl = g1_fixed_table();
   if (ctx) {
+    CTX_LOCK(ctx);
     HC(hipSetDevice(ctx->device));
     ctx->reset_staging();
     uint32_t* d_tau = ctx->scal(&tau, 1);
@@ -1109,8 +1352,9 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
               uint8_t* const* mont_t, uint8_t* commitments_out, uint8_t* evaluations_out) {
   API_BEGIN
   if (!ctx || !evals_f || !evals_t || !commitments_out || !evaluations_out) throw KgsError(KGS_E_ARG, "NULL argument");
+  CTX_LOCK(ctx);
   if ((sel_f == nullptr) != (sel_t == nullptr)) throw KgsError(KGS_E_ARG, "selectors must be both given or both NULL");
-  if (npols < 1 || npols > 10 || nbits < 1 || nbits > 28) throw KgsError(KGS_E_ARG, "bad shape");
+  if (npols < 1 || npols > KGS_MAX_POLS || nbits < 1 || nbits > 28) throw KgsError(KGS_E_ARG, "bad shape");
   HC(hipSetDevice(ctx->device));
   const uint64_t n = 1ull << nbits;
   const size_t E = 32 * n;
@@ -1179,8 +1423,9 @@ int kgs_prove_device(kgs_ctx_t* ctx, int kind, int nbits, int npols, const void*
                      uint8_t* evaluations_out) {
   API_BEGIN
   if (!ctx || !d_evals_f || !d_evals_t || !commitments_out || !evaluations_out) throw KgsError(KGS_E_ARG, "NULL argument");
+  CTX_LOCK(ctx);
   if ((d_sel_f == nullptr) != (d_sel_t == nullptr)) throw KgsError(KGS_E_ARG, "selectors must be both given or both NULL");
-  if (npols < 1 || npols > 10 || nbits < 1 || nbits > 28) throw KgsError(KGS_E_ARG, "bad shape");
+  if (npols < 1 || npols > KGS_MAX_POLS || nbits < 1 || nbits > 28) throw KgsError(KGS_E_ARG, "bad shape");
   HC(hipSetDevice(ctx->device));
   ProveIn in;
   in.kind = kind;
@@ -1198,6 +1443,7 @@ int kgs_prove_device(kgs_ctx_t* ctx, int kind, int nbits, int npols, const void*
 
 int kgs_last_timing(kgs_ctx_t* ctx, double* rounds_ms, int max_rounds) {
   if (!ctx || !rounds_ms) return KGS_E_ARG;
+  CTX_LOCK(ctx);
   int n = (int)ctx->timing.size() < max_rounds ? (int)ctx->timing.size() : max_rounds;
   for (int i = 0; i < n; i++) rounds_ms[i] = ctx->timing[i];
   return n;
@@ -1205,6 +1451,8 @@ int kgs_last_timing(kgs_ctx_t* ctx, double* rounds_ms, int max_rounds) {
 
 int kgs_fr_to_mont(kgs_ctx_t* ctx, const uint8_t* in_std, uint8_t* out_mont, uint64_t n) {
   API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
   uint32_t* a = ctx->buf("prim_a", 32 * n);
   uint32_t* b = ctx->buf("prim_b", 32 * n);
@@ -1218,6 +1466,8 @@ int kgs_fr_to_mont(kgs_ctx_t* ctx, const uint8_t* in_std, uint8_t* out_mont, uin
 
 int kgs_ntt(kgs_ctx_t* ctx, const uint8_t* in_mont, uint8_t* out_mont, int logm, int inverse) {
   API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
   if (logm < 0 || logm > 28) throw KgsError(KGS_E_ARG, "bad logm");
   if (logm > ctx->logM) ensure_domain(*ctx, logm);
@@ -1240,6 +1490,8 @@ int kgs_ntt(kgs_ctx_t* ctx, const uint8_t* in_mont, uint8_t* out_mont, int logm,
 
 int kgs_msm(kgs_ctx_t* ctx, const uint8_t* scalars_mont, uint64_t n, uint8_t out_lem[64]) {
   API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
   if (n > ctx->tb.npts) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
   ctx->reset_staging();
@@ -1255,6 +1507,7 @@ int kgs_msm(kgs_ctx_t* ctx, const uint8_t* scalars_mont, uint64_t n, uint8_t out
 int kgs_ctx_set_shard(kgs_ctx_t* ctx, int rank, int world, kgs_allgather_fn fn, void* user) {
   API_BEGIN
   if (!ctx) throw KgsError(KGS_E_ARG, "ctx is NULL");
+  CTX_LOCK(ctx);
   if (world < 1 || rank < 0 || rank >= world) throw KgsError(KGS_E_ARG, "bad shard rank/world");
   if (world > 1 && !fn) throw KgsError(KGS_E_ARG, "sharding needs an all-gather callback");
   ctx->shard_rank = world > 1 ? rank : 0;
@@ -1267,6 +1520,7 @@ int kgs_ctx_set_shard(kgs_ctx_t* ctx, int rank, int world, kgs_allgather_fn fn, 
 int kgs_ctx_set_msm_lanes(kgs_ctx_t* ctx, int lanes) {
   API_BEGIN
   if (!ctx || lanes < 1 || lanes > 2) throw KgsError(KGS_E_ARG, "msm lanes must be 1 or 2");
+  CTX_LOCK(ctx);
   ctx->msm_lanes = lanes;
   API_END
 }
@@ -1288,6 +1542,8 @@ int kgs_msm_combine(const uint8_t* T_all, int nparts, int c, uint8_t out_lem[64]
 int kgs_grand_build(kgs_ctx_t* ctx, int kind, const uint8_t* f_mont, const uint8_t* t_mont, const uint8_t* sel_f,
                     const uint8_t* sel_t, const uint8_t gamma_mont[32], uint64_t n, uint8_t* out_mont) {
   API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
   if ((sel_f == nullptr) != (sel_t == nullptr)) throw KgsError(KGS_E_ARG, "selectors must be both given or both NULL");
   ctx->reset_staging();
@@ -1327,6 +1583,8 @@ int kgs_grand_build(kgs_ctx_t* ctx, int kind, const uint8_t* f_mont, const uint8
 int kgs_poly_eval(kgs_ctx_t* ctx, const uint8_t* coef_mont, uint64_t len, const uint8_t x_mont[32],
                   uint8_t out_mont[32]) {
   API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
   ctx->reset_staging();
   uint32_t* a = ctx->buf("prim_a", 32 * (len ? len : 1));
@@ -1341,6 +1599,8 @@ int kgs_poly_eval(kgs_ctx_t* ctx, const uint8_t* coef_mont, uint64_t len, const 
 int kgs_poly_div_x_sub(kgs_ctx_t* ctx, const uint8_t* coef_mont, uint64_t len, const uint8_t z_mont[32],
                        uint8_t* out_mont) {
   API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
   if (len < 2) throw KgsError(KGS_E_ARG, "length must be >= 2");
   ctx->reset_staging();
@@ -1370,6 +1630,8 @@ int kgs_keccak256(const uint8_t* data, uint64_t len, uint8_t out[32]) {
 
 int kgs_bench_msm(kgs_ctx_t* ctx, const void* d_scalars_mont, uint64_t n, int reps, double* ms) {
   API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
   if (n > ctx->tb.npts) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
   uint32_t* dT = ctx->buf("msm_T", (size_t)64 * ctx->tb.c * 128);
@@ -1392,6 +1654,8 @@ int kgs_bench_msm(kgs_ctx_t* ctx, const void* d_scalars_mont, uint64_t n, int re
 int kgs_bench_msm_phases(kgs_ctx_t* ctx, const void* d_scalars_mont, uint64_t n, int reps, double* phase_ms,
                          uint64_t* entries) {
   API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
   if (n > ctx->tb.npts) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
   uint32_t* dT = ctx->buf("msm_T", (size_t)64 * ctx->tb.c * 128);
@@ -1417,6 +1681,8 @@ int kgs_bench_msm_phases(kgs_ctx_t* ctx, const void* d_scalars_mont, uint64_t n,
 
 int kgs_bench_ntt(kgs_ctx_t* ctx, void* d_buf, int logm, int reps, double* ms) {
   API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
   if (logm > ctx->logM) ensure_domain(*ctx, logm);
   uint32_t* a = (uint32_t*)d_buf;

@@ -125,6 +125,38 @@ static napi_value CtxCreate(napi_env env, napi_callback_info info) {
   return ext;
 }
 
+// deviceCount() -> number of visible HIP devices
+static napi_value DeviceCount(napi_env env, napi_callback_info) {
+  int n = 0;
+  if (kgs_device_count(&n) != KGS_OK) {
+    napi_throw_error(env, nullptr, kgs_last_error());
+    return nullptr;
+  }
+  napi_value v;
+  napi_create_int32(env, n, &v);
+  return v;
+}
+
+// ptauPower(path) -> power from the ptau header (readPTauHeader, src/ptau_utils.js:3-24)
+static napi_value PtauPower(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  size_t len = 0;
+  napi_get_value_string_utf8(env, argv[0], nullptr, 0, &len);
+  std::string path(len + 1, '\0');
+  napi_get_value_string_utf8(env, argv[0], &path[0], len + 1, &len);
+  path.resize(len);
+  int power = 0;
+  if (kgs_ptau_power(path.c_str(), &power) != KGS_OK) {
+    napi_throw_error(env, nullptr, kgs_last_error());
+    return nullptr;
+  }
+  napi_value v;
+  napi_create_int32(env, power, &v);
+  return v;
+}
+
 // keccak256(Uint8Array) -> Uint8Array(32)
 static napi_value Keccak(napi_env env, napi_callback_info info) {
   size_t argc = 1;
@@ -350,6 +382,8 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"prove", nullptr, Prove, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"keccak256", nullptr, Keccak, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"verifyPtau", nullptr, VerifyPtau, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"ptauPower", nullptr, PtauPower, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(desc) / sizeof(desc[0]), desc);
   return exports;

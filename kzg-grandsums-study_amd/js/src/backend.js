@@ -1,5 +1,20 @@
-// Device backend: one libkgs context per HIP device, device-resident SRS cached per ptau path.
+// Device backend: a pool of libkgs contexts spread over the visible HIP devices.
+//
+// The reference prover is an independent async function per call
+// (src/grandsum/mset_eq_kzg_prover.js:12): `Promise.all([prover(a), prover(b)])` runs both. Here
+// every call takes a context slot for its whole duration (SRS load + prove), so a context is never
+// used by two calls at once, and independent calls run concurrently on different contexts (each
+// with its own HIP stream and buffers, on the same GPU or on another one). libkgs additionally
+// serialises calls per context with a mutex, and shares the read-only SRS / NTT tables between the
+// contexts of a device, so a pool of several contexts costs one set of tables per GPU.
+//
+// Knobs: KGS_JS_CONTEXTS = contexts per device (default 4: the proofs in flight that keep one
+// MI355X busy), KGS_DEVICES = comma-separated device list (default: every visible device).
 const path = require("path");
+
+// N-API async work runs on the libuv thread pool (4 threads by default): one thread per context of
+// an 8-GPU pool needs more. Effective only if set before the process first uses the pool.
+if (!process.env.UV_THREADPOOL_SIZE) process.env.UV_THREADPOOL_SIZE = "64";
 
 let addon = null;
 function load() {
@@ -10,28 +25,73 @@ function load() {
     return addon;
 }
 
-const contexts = new Map();
-const loaded = new Map();
-
-async function context(device = 0) {
-    const a = load();
-    if (!contexts.has(device)) contexts.set(device, a.ctxCreate(device));
-    return contexts.get(device);
+function devices() {
+    const env = process.env.KGS_DEVICES;
+    if (env && env.trim() !== "") return env.split(",").map(x => parseInt(x, 10)).filter(x => x >= 0);
+    const n = load().deviceCount();
+    if (n < 1) throw new Error("no HIP device visible");
+    return Array.from({ length: n }, (_, i) => i);
 }
 
-async function loadPtau(ctx, pTauFilename) {
-    const key = path.resolve(pTauFilename);
-    if (loaded.get(ctx) !== key) {
-        await load().srsLoadPtau(ctx, key, -1);
-        loaded.set(ctx, key);
+function perDevice() {
+    const v = parseInt(process.env.KGS_JS_CONTEXTS || "4", 10);
+    return Number.isFinite(v) && v >= 1 ? v : 4;
+}
+
+const pool = { slots: [], idle: [], waiters: [], devs: null, cap: 0 };
+
+function newSlot() {
+    if (!pool.devs) {
+        pool.devs = devices();
+        pool.cap = pool.devs.length * perDevice();
     }
-    return load().srsInfo(ctx);
+    // round-robin over devices: slot i lives on device devs[i % ndev]
+    const device = pool.devs[pool.slots.length % pool.devs.length];
+    const slot = { device, ctx: load().ctxCreate(device), index: pool.slots.length };
+    pool.slots.push(slot);
+    return slot;
 }
 
-async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT, device = 0) {
-    const ctx = await context(device);
-    await loadPtau(ctx, pTauFilename);
-    return load().prove(ctx, kind, nBits, evalsF, evalsT, selF, selT);
+function acquire() {
+    if (pool.idle.length) return Promise.resolve(pool.idle.pop());
+    if (!pool.devs || pool.slots.length < pool.cap) return Promise.resolve(newSlot());
+    return new Promise(resolve => pool.waiters.push(resolve));
 }
 
-module.exports = { load, context, loadPtau, prove, GRANDSUM: 0, GRANDPRODUCT: 1 };
+function release(slot) {
+    const w = pool.waiters.shift();
+    if (w) w(slot);
+    else pool.idle.push(slot);
+}
+
+// run fn(slot) with exclusive use of one context
+async function withContext(fn) {
+    const slot = await acquire();
+    try {
+        return await fn(slot);
+    } finally {
+        release(slot);
+    }
+}
+
+// ptau header power, read without a context (readPTauHeader, src/ptau_utils.js:3-24)
+function ptauPower(pTauFilename) {
+    return load().ptauPower(path.resolve(pTauFilename));
+}
+
+// SRS load (only 2^(nBits+1) points, as prover.js:83-85 reads; grow-only device cache in libkgs)
+// and prove on the same held context: nothing can swap the SRS between the two
+async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT) {
+    const key = path.resolve(pTauFilename);
+    return withContext(async slot => {
+        await load().srsLoadPtau(slot.ctx, key, nBits);
+        return load().prove(slot.ctx, kind, nBits, evalsF, evalsT, selF, selT);
+    });
+}
+
+function poolInfo() {
+    return { contexts: pool.slots.length, capacity: pool.cap, devices: pool.devs ? pool.devs.slice() : null,
+             idle: pool.idle.length, waiting: pool.waiters.length };
+}
+
+module.exports = { load, ptauPower, prove, withContext, poolInfo, GRANDSUM: 0, GRANDPRODUCT: 1 };

@@ -6,6 +6,8 @@ const { Evaluations } = require("./polynomial/evaluations");
 const { getCurveFromName } = require("./curve");
 
 async function prove(kind, pTauFilename, evalsFs, evalsTs, evalsSelF, evalsSelT) {
+    // the ptau header is read first, as the reference does (prover.js:15-16)
+    const nBitsPTau = backend.ptauPower(pTauFilename);
     const curve = await getCurveFromName("bn128");
     if (!Array.isArray(evalsFs)) evalsFs = [evalsFs];
     if (!Array.isArray(evalsTs)) evalsTs = [evalsTs];
@@ -38,9 +40,7 @@ async function prove(kind, pTauFilename, evalsFs, evalsTs, evalsSelF, evalsSelT)
     }
     const nBits = Math.ceil(Math.log2(evalsFs[0].length()));
     if (evalsFs[0].length() !== 2 ** nBits) throw new Error("Polynomial length must be a power of two.");
-    const ctx = await backend.context(0);
-    const { power } = await backend.loadPtau(ctx, pTauFilename);
-    if (power < nBits) throw new Error("The Powers of Tau file is not sufficiently large to commit the polynomials.");
+    if (nBitsPTau < nBits) throw new Error("The Powers of Tau file is not sufficiently large to commit the polynomials.");
 
     const res = await backend.prove(kind, pTauFilename, nBits,
         evalsFs.map(e => e.eval), evalsTs.map(e => e.eval),

@@ -1,5 +1,7 @@
 // Test driver used by tests/test_js_dropin.py: read {ptau, cases:[{kind, F:[hex], T:[hex], selF, selT}]}
 // from argv[2], run the drop-in provers, print {proofs:[{commitments:{k:hex}, evaluations:{k:hex}, montF:[hex]}]}.
+// With spec.concurrent every case is started at once (Promise.all), as independent reference calls
+// would be (src/grandsum/mset_eq_kzg_prover.js:12 is an independent async function per call).
 const fs = require("fs");
 const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_grandproduct_prover } = require("../index");
 
@@ -8,8 +10,7 @@ const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_
     const curve = await getCurveFromName("bn128");
     const hex = b => Buffer.from(b).toString("hex");
     const ev = h => new Evaluations(new Uint8Array(Buffer.from(h, "hex")), curve);
-    const out = [];
-    for (const c of spec.cases) {
+    const one = async c => {
         const F = c.F.map(ev), T = c.T.map(ev);
         const fn = c.kind === "grandsum" ? mset_eq_kzg_grandsum_prover : mset_eq_kzg_grandproduct_prover;
         try {
@@ -18,10 +19,18 @@ const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_
             const o = { commitments: {}, evaluations: {}, montF: F.map(e => hex(e.eval)) };
             for (const k of Object.keys(proof.commitments)) o.commitments[k] = hex(proof.commitments[k]);
             for (const k of Object.keys(proof.evaluations)) o.evaluations[k] = hex(proof.evaluations[k]);
-            out.push(o);
+            return o;
         } catch (e) {
-            out.push({ error: e.message });
+            return { error: e.message };
         }
+    };
+    let out;
+    if (spec.concurrent) {
+        out = await Promise.all(spec.cases.map(one));
+    } else {
+        out = [];
+        for (const c of spec.cases) out.push(await one(c));
     }
-    console.log(JSON.stringify({ proofs: out }));
+    const { poolInfo } = require("../src/backend");
+    console.log(JSON.stringify({ proofs: out, pool: poolInfo() }));
 })().catch(e => { console.error(e); process.exit(1); });

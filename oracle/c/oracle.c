@@ -693,3 +693,64 @@ int orc_max_threads(void) {
   return 1;
 #endif
 }
+
+/* p(x) from the evaluations of p on <w_n> (natural order), standard-form 32 B LE in and out:
+ * p(x) = (x^n - 1)/n * sum_i e_i w^i / (x - w^i) (barycentric; x not in <w_n>). Test checker for the
+ * transcript-independent commitments of large proofs: C(F) == F(tau) G1 (tests/test_gpu_configs.py).
+ * Chunked Montgomery batch inversion, one chunk per thread. */
+int orc_eval_evals_std(const uint8_t* evals_std, int nbits, const uint8_t x_std[32], uint8_t out_std[32]) {
+  const uint64_t n = 1ull << nbits;
+  uint64_t xs[4];
+  memcpy(xs, x_std, 32);
+  const fe x = f_from_std(&FR, xs);
+  const fe w = fr_w(nbits);
+  int nth = 1;
+#ifdef _OPENMP
+  nth = omp_get_max_threads();
+#endif
+  if ((uint64_t)nth > n) nth = (int)n;
+  fe* part = (fe*)calloc(nth, sizeof(fe));
+  int bad = 0;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nth) reduction(| : bad)
+#endif
+  {
+    int t = 0;
+#ifdef _OPENMP
+    t = omp_get_thread_num();
+#endif
+    const uint64_t lo = n * t / nth, hi = n * (t + 1) / nth, m = hi - lo;
+    uint64_t e[4] = {lo, 0, 0, 0};
+    fe wi = f_pow(&FR, w, e);  /* w^lo */
+    fe* den = (fe*)malloc(sizeof(fe) * (m ? m : 1));
+    fe* wp = (fe*)malloc(sizeof(fe) * (m ? m : 1));
+    for (uint64_t i = 0; i < m; i++) {
+      wp[i] = wi;
+      den[i] = RS(x, wi);
+      if (f_is0(den[i])) bad = 1;
+      wi = RM(wi, w);
+    }
+    if (m == 0) den[0] = f_zero();
+    fe* inv = batch_inverse(den, m);
+    fe s = f_zero();
+    for (uint64_t i = 0; i < m; i++) {
+      uint64_t v[4];
+      memcpy(v, evals_std + 32 * (lo + i), 32);
+      s = RA(s, RM(RM(f_from_std(&FR, v), wp[i]), inv[i]));
+    }
+    part[t] = s;
+    free(den); free(wp); free(inv);
+  }
+  if (bad) { free(part); return -1; }
+  fe s = f_zero();
+  for (int t = 0; t < nth; t++) s = RA(s, part[t]);
+  free(part);
+  uint64_t en[4] = {n, 0, 0, 0};
+  fe xn = f_pow(&FR, x, en);
+  fe scale = RM(RS(xn, f_one(&FR)), f_inv(&FR, f_from_u64(&FR, n)));
+  fe r = RM(scale, s);
+  uint64_t o[4];
+  f_to_std(&FR, r, o);
+  memcpy(out_std, o, 32);
+  return 0;
+}

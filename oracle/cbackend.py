@@ -30,8 +30,18 @@ def lib():
         L.orc_msm.restype = None
         L.orc_keccak256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
         L.orc_keccak256.restype = None
+        L.orc_eval_evals_std.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p]
         _lib = L
     return _lib
+
+
+def eval_evals_std(evals_std, nbits, x):
+    """p(x) (int) from p's standard-form evaluations on <w_n> (barycentric, OpenMP)."""
+    out = ctypes.create_string_buffer(32)
+    rc = lib().orc_eval_evals_std(evals_std, nbits, int(x).to_bytes(32, "little"), out)
+    if rc != 0:
+        raise ValueError("x lies in the evaluation domain")
+    return int.from_bytes(out.raw, "little")
 
 
 def load_srs_bytes(ptau_path):

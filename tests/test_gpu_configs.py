@@ -1,0 +1,262 @@
+"""GPU tests of BASELINE.json's large configurations and of the boundary's robustness.
+
+configs[2] (grand-product n=2^20), configs[3] (grand-sum n=2^24) and configs[4] (selected-vector
+grand-sum n=2^22, k=4) run through the HIP path (C-ABI kgs_prove, the host-buffer drop-in boundary)
+and are checked by size-independent properties, with no full-size CPU oracle run:
+  * the proof verifies: native verifier (kgs_verify_ptau: transcript replay + optimal-ate pairing)
+    AND the oracle's restated verifier in trapdoor form (tau·A == B);
+  * the transcript-independent commitment C(F0) equals F0(tau)·G1, F0(tau) evaluated from the
+    evaluations by the C oracle (barycentric, OpenMP) — an independent check of round 1's iNTT + MSM;
+  * selector commitments equal their closed form (1 - L_{n-1}(tau))·G1 and (1 - L_0(tau))·G1;
+  * determinism (a second proof of the same inputs is byte-identical).
+MSM point-range sharding is checked at 2^22 with 2 and 8 simulated ranks (ThreadGroup, one context
+per rank on cuda:0): every rank's proof is byte-identical to the unsharded one.
+Reference: test/mset_eq_kzg_grandsum.test.js:80-104, test/mset_eq_kzg_grandproduct.test.js.
+"""
+import os
+import random
+import threading
+
+import numpy as np
+import pytest
+
+import common
+from oracle import bn254 as bn
+from oracle import protocol as P
+from oracle.ptau import PTau
+
+pytestmark = pytest.mark.gpu
+R = bn.R
+
+
+@pytest.fixture(scope="module")
+def K():
+    return common.load_pkg()
+
+
+def gpu_ptau(K, nbits):
+    """Synthetic ptau of power nbits written by the product's GPU writer (byte-identical to the
+    oracle's writer: test_gpu_parity.py::test_synthetic_ptau_writer_matches_oracle)."""
+    path = f"/tmp/kgs_test_gpu_p{nbits}.ptau"
+    if not os.path.exists(path):
+        c = K.Context(0)
+        tmp = f"{path}.{os.getpid()}"
+        c.write_synthetic_ptau(tmp, nbits, common.tau())
+        c.close()
+        os.replace(tmp, path)
+    return path
+
+
+def np_inputs(seed, nbits, npols, selected):
+    """Same shapes as common.make_inputs (T = F rotated by one; selectors ones but the last / the
+    first), generated with numpy so that 2^24 elements take seconds: F_i < 2^253 < r."""
+    n = 1 << nbits
+    rng = np.random.Generator(np.random.PCG64(seed))
+    Fs, Ts = [], []
+    for _ in range(npols):
+        w = rng.integers(0, np.iinfo(np.uint64).max, size=(n, 4), dtype=np.uint64, endpoint=True)
+        w[:, 3] &= np.uint64((1 << 61) - 1)
+        f = np.ascontiguousarray(w).view(np.uint8).reshape(n, 32)
+        Fs.append(f.tobytes())
+        Ts.append(np.roll(f, 1, axis=0).tobytes())
+    sF = sT = None
+    if selected:
+        one = np.frombuffer(common.mont_bytes([1]), dtype=np.uint8)
+        a = np.tile(one, n)
+        b = a.copy()
+        a[32 * (n - 1):] = 0
+        b[:32] = 0
+        sF, sT = a.tobytes(), b.tobytes()
+    return Fs, Ts, sF, sT
+
+
+def private_copy(path):
+    import shutil
+    dst = f"{path}.private{os.getpid()}.ptau"
+    if not os.path.exists(dst):
+        shutil.copyfile(path, dst)
+    return dst
+
+
+def lagrange_at(j, nbits, x):
+    n = 1 << nbits
+    wj = pow(bn.FR_W[nbits], j, R)
+    return wj * (pow(x, n, R) - 1) % R * pow(n * (x - wj) % R, R - 2, R) % R
+
+
+def g1(s):
+    return bn.g1_to_lem(bn.g1_mul(bn.G1_GEN, s % R))
+
+
+def check_large(K, kind, nbits, npols, sel, seed):
+    from oracle import cbackend as C
+    path = gpu_ptau(K, nbits)
+    ctx = K.Context(0)
+    ctx.load_ptau(path, nbits)
+    Fs, Ts, sF, sT = np_inputs(seed, nbits, npols, sel)
+    kk = K.GRANDSUM if kind == "grandsum" else K.GRANDPRODUCT
+    coms, evs, _, _ = ctx.prove(kk, nbits, Fs, Ts, sF, sT, mont_out=False)
+    cn, en = K.proof_names(kk, npols, sel)
+    proof = {"commitments": dict(zip(cn, coms)), "evaluations": dict(zip(en, evs))}
+    # 1. verifies: native pairing verifier and the oracle's verifier (trapdoor form, no ptau read)
+    vf = K.grandsum_verifier if kind == "grandsum" else K.grandproduct_verifier
+    assert vf(path, proof, nbits) is True
+    assert P.verify(kind, PTau.__new__(PTau), proof, nbits, tau=common.tau())
+    # 2. C(F0) == F0(tau) G1 with F0(tau) from the C oracle
+    tau = common.tau()
+    f0 = C.eval_evals_std(Fs[0], nbits, tau)
+    assert proof["commitments"]["F0" if npols > 1 else "F"] == g1(f0)
+    t_last = C.eval_evals_std(Ts[-1], nbits, tau)
+    assert proof["commitments"][f"T{npols - 1}" if npols > 1 else "T"] == g1(t_last)
+    # 3. selector commitments in closed form
+    if sel:
+        assert proof["commitments"]["selF"] == g1(1 - lagrange_at((1 << nbits) - 1, nbits, tau))
+        assert proof["commitments"]["selT"] == g1(1 - lagrange_at(0, nbits, tau))
+    # 4. determinism
+    coms2, evs2, _, _ = ctx.prove(kk, nbits, Fs, Ts, sF, sT, mont_out=False)
+    assert coms2 == coms and evs2 == evs
+    ctx.close()
+    return proof
+
+
+def test_c3_grandproduct_2p20(K):
+    """BASELINE configs[2]: grand-product n = 2^20, k = 1 (test/mset_eq_kzg_grandproduct.test.js)."""
+    check_large(K, "grandproduct", 20, 1, False, 0xC3)
+
+
+def test_c4_grandsum_2p24(K):
+    """BASELINE configs[3]: grand-sum n = 2^24, k = 1, one GPU."""
+    check_large(K, "grandsum", 24, 1, False, 0xC4)
+
+
+def test_c5_selected_vector_2p22_k4(K):
+    """BASELINE configs[4]: selected-vector grand-sum n = 2^22, k = 4 (the lookup config's shape)."""
+    check_large(K, "grandsum", 22, 4, True, 0xC5)
+
+
+def _sharded(K, world, ptau, nbits, kind, Fs, Ts, sF, sT):
+    grp = K.ThreadGroup(world)
+    ctxs = [K.Context(0) for _ in range(world)]
+    for r, c in enumerate(ctxs):
+        c.load_ptau(ptau, nbits)
+        c.set_shard(r, world, grp.allgather(r))
+        c.set_msm_lanes(1)
+    out, err = [None] * world, [None] * world
+
+    def run(r):
+        try:
+            out[r] = ctxs[r].prove(kind, nbits, Fs, Ts, sF, sT, mont_out=False)[:2]
+        except Exception as e:  # pragma: no cover
+            err[r] = e
+            grp._bar.abort()
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    for c in ctxs:
+        c.close()
+    assert not any(err), err
+    return out
+
+
+@pytest.mark.parametrize("world,npols,sel", [(2, 1, False), (8, 4, True)])
+def test_sharded_2p22(K, world, npols, sel):
+    """configs[3]/[4]'s multi-GPU split rehearsed on one GPU: every commitment MSM point-range
+    sharded over `world` ranks; all ranks' proofs == the unsharded proof, byte for byte."""
+    nbits = 22
+    path = gpu_ptau(K, nbits)
+    Fs, Ts, sF, sT = np_inputs(0x5A + world, nbits, npols, sel)
+    ctx = K.Context(0)
+    ctx.load_ptau(path, nbits)
+    want = ctx.prove(K.GRANDSUM, nbits, Fs, Ts, sF, sT, mont_out=False)[:2]
+    ctx.close()
+    got = _sharded(K, world, path, nbits, K.GRANDSUM, Fs, Ts, sF, sT)
+    for r in range(world):
+        assert got[r] == want, r
+
+
+def test_srs_loaded_by_need(K):
+    """The drop-in prover loads only the 2^(nBits+1) points a proof commits with
+    (src/grandsum/mset_eq_kzg_prover.js:83-85), growing on demand, never shrinking."""
+    ptau = private_copy(common.oracle_ptau(9))  # no other context shares this file's tables
+    srs = P.SRS(ptau, common.tau())
+    old = K._CTX.pop(0, None)
+    if old is not None:
+        old.close()
+    ctx = K._context(0)
+    for nbits, expect_pts in ((5, 64), (7, 256), (5, 256)):
+        Fs, Ts, _, _ = common.make_inputs(70 + nbits, nbits, 1, False)
+        got = K.grandsum_prover(ptau, K.Evaluations(Fs[0]), K.Evaluations(Ts[0]))
+        assert got == P.prove("grandsum", srs, P.EvalBuffer(Fs[0]), P.EvalBuffer(Ts[0]))
+        power, npts, _ = ctx.srs_info()
+        assert power == 9 and npts == expect_pts, (nbits, npts)
+
+
+@pytest.mark.parametrize("kind", ["grandsum", "grandproduct"])
+@pytest.mark.parametrize("sel", [False, True])
+def test_twelve_multisets(K, kind, sel):
+    """k = 12 vectors (above the 10 of round 1; the reference bounds nPols nowhere): byte-exact vs
+    the oracle — linear combinations and evaluation batches run in several launches."""
+    nbits, k = 3, 12
+    ptau = common.oracle_ptau(9)
+    srs = P.SRS(ptau, common.tau())
+    Fs, Ts, sF, sT = common.make_inputs(1200 + sel, nbits, k, sel)
+    fn = K.grandsum_prover if kind == "grandsum" else K.grandproduct_prover
+    got = fn(ptau, [K.Evaluations(x) for x in Fs], [K.Evaluations(x) for x in Ts],
+             K.Evaluations(sF) if sel else None, K.Evaluations(sT) if sel else None)
+    exp = P.prove(kind, srs, [P.EvalBuffer(x) for x in Fs], [P.EvalBuffer(x) for x in Ts],
+                  P.EvalBuffer(sF) if sel else None, P.EvalBuffer(sT) if sel else None)
+    assert got == exp
+    assert (K.grandsum_verifier if kind == "grandsum" else K.grandproduct_verifier)(ptau, got, nbits) is True
+
+
+def test_failed_load_leaves_context_usable(K, monkeypatch):
+    """A device allocation failure while loading an SRS leaves the context without an SRS (not with
+    a half-built one); loading a smaller one afterwards works and proves correctly."""
+    ptau9 = common.oracle_ptau(9)
+    ctx = K.Context(0)
+    Fs, Ts, sF, sT = common.make_inputs(77, 4, 1, False)
+    ctx.load_ptau(ptau9, 4)
+    want = ctx.prove(K.GRANDSUM, 4, Fs, Ts, sF, sT, mont_out=False)[:2]
+    ptau14 = private_copy(gpu_ptau(K, 14))
+    monkeypatch.setenv("KGS_DEBUG_ALLOC_LIMIT", str(4 << 20))  # the 2^15-point table needs > 4 MiB
+    with pytest.raises(K.KgsError):
+        ctx.load_ptau(ptau14, 14)
+    monkeypatch.delenv("KGS_DEBUG_ALLOC_LIMIT")
+    with pytest.raises(K.KgsError, match="no SRS loaded"):
+        ctx.prove(K.GRANDSUM, 4, Fs, Ts, sF, sT, mont_out=False)
+    ctx.load_ptau(ptau9, 4)
+    assert ctx.prove(K.GRANDSUM, 4, Fs, Ts, sF, sT, mont_out=False)[:2] == want
+    ctx.close()
+
+
+def test_one_context_many_threads(K):
+    """Calls on ONE context from several threads are serialised by the context's mutex: every
+    proof is right (round 1 had no lock; concurrent calls raced on the pool and streams)."""
+    ptau = common.oracle_ptau(9)
+    srs = P.SRS(ptau, common.tau())
+    ctx = K.Context(0)
+    ctx.load_ptau(ptau, 6)
+    cases = [common.make_inputs(300 + i, 6, 1 + i % 2, i % 3 == 0) for i in range(8)]
+    kinds = [K.GRANDSUM if i % 2 == 0 else K.GRANDPRODUCT for i in range(8)]
+    out = [None] * 8
+
+    def run(i):
+        Fs, Ts, sF, sT = cases[i]
+        out[i] = ctx.prove(kinds[i], 6, Fs, Ts, sF, sT, mont_out=False)[:2]
+    th = [threading.Thread(target=run, args=(i,)) for i in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    for i in range(8):
+        Fs, Ts, sF, sT = cases[i]
+        kind = "grandsum" if kinds[i] == K.GRANDSUM else "grandproduct"
+        k = len(Fs)
+        exp = P.prove(kind, srs, [P.EvalBuffer(x) for x in Fs] if k > 1 else P.EvalBuffer(Fs[0]),
+                      [P.EvalBuffer(x) for x in Ts] if k > 1 else P.EvalBuffer(Ts[0]),
+                      P.EvalBuffer(sF) if sF else None, P.EvalBuffer(sT) if sT else None)
+        cn, en = K.proof_names(kinds[i], k, sF is not None)
+        assert out[i] == ([exp["commitments"][c] for c in cn], [exp["evaluations"][e] for e in en]), i
+    ctx.close()

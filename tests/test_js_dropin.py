@@ -72,6 +72,37 @@ def test_js_proofs_match_oracle(tmp_path):
 
 
 @pytest.mark.gpu
+def test_js_concurrent_provers_match_oracle(tmp_path):
+    """12 prover() Promises in flight at once (Promise.all), grand-sum and grand-product mixed, 1-3
+    vectors, with and without selectors, two domain sizes: every proof byte-identical to the oracle
+    (the reference's provers are independent async calls, src/grandsum/mset_eq_kzg_prover.js:12)."""
+    ptau = common.oracle_ptau(9)
+    srs = P.SRS(ptau, common.tau())
+    cases, expect = [], []
+    for i in range(12):
+        kind = "grandsum" if i % 2 == 0 else "grandproduct"
+        npols, sel, nbits = 1 + i % 3, i % 4 >= 2, 5 + (i % 5 == 0) * 2
+        Fs, Ts, sF, sT = common.make_inputs(7000 + i, nbits, npols, sel)
+        cases.append({"kind": kind, "F": [x.hex() for x in Fs], "T": [x.hex() for x in Ts],
+                      "selF": sF.hex() if sF else None, "selT": sT.hex() if sT else None})
+        eF = [P.EvalBuffer(x) for x in Fs]
+        eT = [P.EvalBuffer(x) for x in Ts]
+        pr = P.prove(kind, srs, eF if npols > 1 else eF[0], eT if npols > 1 else eT[0],
+                     P.EvalBuffer(sF) if sF else None, P.EvalBuffer(sT) if sT else None)
+        expect.append({sec: {k: v.hex() for k, v in pr[sec].items()} for sec in ("commitments", "evaluations")})
+    spec = tmp_path / "spec.json"
+    spec.write_text(json.dumps({"ptau": ptau, "cases": cases, "concurrent": True}))
+    env = dict(os.environ, KGS_JS_CONTEXTS="4")
+    out = json.loads(subprocess.check_output([NODE, os.path.join(JS, "test", "prove_from_json.js"), str(spec)],
+                                             timeout=600, env=env))
+    for i, (got, exp) in enumerate(zip(out["proofs"], expect)):
+        assert "error" not in got, (i, got)
+        assert {"commitments": got["commitments"], "evaluations": got["evaluations"]} == exp, i
+    # the calls really overlapped: the pool grew to its capacity
+    assert out["pool"]["contexts"] == 4 and out["pool"]["waiting"] == 0
+
+
+@pytest.mark.gpu
 def test_reference_style_cases():
     out = subprocess.check_output([NODE, os.path.join(JS, "test", "reference_style.test.js"), common.oracle_ptau(9)],
                                   timeout=600)
