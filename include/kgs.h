@@ -143,7 +143,9 @@ int kgs_verify(int kind, int nbits, int npols, int selected, const uint8_t* comm
 int kgs_verify_ptau(int kind, const char* ptau_path, int nbits, int npols, int selected, const uint8_t* commitments,
                     const uint8_t* evaluations);
 
-/* Per-proof timing of the last kgs_prove* call (milliseconds, host wall clock per round). */
+/* Per-proof timing of the last kgs_prove* call (milliseconds, host wall clock): [0..4] prover rounds
+ * 1-5, [5] unused, and for kgs_prove (host buffers) [6] input copy into pinned staging, [7] the
+ * prover, [8] wait for the Montgomery write-back to the caller. Returns the number written. */
 int kgs_last_timing(kgs_ctx_t* ctx, double* rounds_ms, int max_rounds);
 
 /* ---- primitives (host buffers in/out; used by tests and by the bench's roofline legs) ---- */

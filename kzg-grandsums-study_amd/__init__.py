@@ -328,8 +328,8 @@ class Context:
         return out.raw
 
     def last_timing(self):
-        arr = (ctypes.c_double * 8)()
-        n = lib().kgs_last_timing(self._h, arr, 8)
+        arr = (ctypes.c_double * 9)()
+        n = lib().kgs_last_timing(self._h, arr, 9)
         return list(arr[:max(n, 0)])
 
     # ---- full prover ----

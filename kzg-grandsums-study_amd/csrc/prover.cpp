@@ -682,7 +682,8 @@ void run_lincomb(hipStream_t st, uint32_t* out, uint64_t n, const LcTerms& t) {
 void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out) {
   using clk = std::chrono::steady_clock;
   auto t0 = clk::now();
-  c.timing.assign(6, 0.0);
+  c.timing.resize(9, 0.0);
+  for (int r = 0; r < 6; r++) c.timing[r] = 0.0;
   auto lap = [&](int r) {
     auto t1 = clk::now();
     c.timing[r] = std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -1386,7 +1387,10 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
     dsts.push_back(ctx->buf("in_sf", E));
     dsts.push_back(ctx->buf("in_st", E));
   }
+  using hclk = std::chrono::steady_clock;
+  const auto h0 = hclk::now();
   par_copy(in_jobs);
+  const auto h1 = hclk::now();
   for (size_t v = 0; v < in_jobs.size(); v++)
     HC(hipMemcpyAsync(dsts[v], in_jobs[v].dst, E, hipMemcpyHostToDevice, ctx->st));
   for (int i = 0; i < npols; i++) {
@@ -1413,8 +1417,16 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
     }
   } out_copy;
   if (!out_jobs.empty()) in.after_round1 = [&] { out_copy.t = std::thread([&] { par_copy(out_jobs); }); };
+  const auto h2 = hclk::now();
   prove_impl(*ctx, in, commitments_out, evaluations_out);  // ends synchronised
+  const auto h3 = hclk::now();
   if (out_copy.t.joinable()) out_copy.t.join();
+  const auto h4 = hclk::now();
+  // host-boundary phases: [6] input copy into pinned staging, [7] prover, [8] write-back wait
+  ctx->timing.resize(9, 0.0);
+  ctx->timing[6] = std::chrono::duration<double, std::milli>(h1 - h0).count();
+  ctx->timing[7] = std::chrono::duration<double, std::milli>(h3 - h2).count();
+  ctx->timing[8] = std::chrono::duration<double, std::milli>(h4 - h3).count();
   API_END
 }
 
