@@ -33,7 +33,12 @@
 #include "host_field.hpp"
 #include "host_pairing.hpp"
 #include "kernels.hpp"
+#include "host_error.hpp"
+#ifndef KGS_NO_ROCTX
+#include <rocprofiler-sdk-roctx/roctx.h>
+#endif
 #include "keccak.hpp"
+#include "ptau_io.hpp"
 #include "transcript.hpp"
 
 using namespace kgs;
@@ -41,13 +46,6 @@ using host::Fq;
 using host::Fr;
 
 namespace {
-
-thread_local std::string g_err;
-
-struct KgsError : std::runtime_error {
-  int code;
-  KgsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
-};
 
 #define HC(x)                                                                                    \
   do {                                                                                           \
@@ -62,6 +60,31 @@ static void check_launch() {
 }
 
 using host::fr_w;
+
+// roctx ranges (rocprofv3 --marker-trace): one per prover round and per host-boundary phase, so a
+// trace shows where a proof's host wall time goes next to its kernels. -DKGS_NO_ROCTX removes them.
+struct Range {
+  bool open = false;
+  explicit Range(const char* name = nullptr) {
+    if (name) push(name);
+  }
+  void push(const char* name) {
+    pop();
+#ifndef KGS_NO_ROCTX
+    roctxRangePushA(name);
+#endif
+    open = true;
+  }
+  void pop() {
+#ifndef KGS_NO_ROCTX
+    if (open) roctxRangePop();
+#endif
+    open = false;
+  }
+  ~Range() { pop(); }
+};
+const char* const ROUND_NAMES[5] = {"kgs.round1.commit_witness", "kgs.round2.grand_poly", "kgs.round3.quotient",
+                                    "kgs.round4.evaluations", "kgs.round5.openings"};
 
 // Every device allocation goes through here. KGS_DEBUG_ALLOC_LIMIT=<bytes> (fault injection for the
 // tests) makes any single request above that size fail as out-of-memory.
@@ -438,7 +461,10 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
       int cc = choose_c(npts);
       int W = (255 + cc - 1) / cc;
       // sorted entries pack j * npts + i into 31 bits (bit 31 = sign): widen the window until it fits
-      while ((uint64_t)W * npts > (1ull << 31) && cc < KGS_C_MAX) W = (255 + (++cc) - 1) / cc;
+      while ((uint64_t)W * npts > (1ull << 31) && cc < KGS_C_MAX) {
+        cc++;
+        W = (255 + cc - 1) / cc;
+      }
       if ((uint64_t)W * npts > (1ull << 31)) throw KgsError(KGS_E_SRS, "SRS too large for the MSM entry index");
       auto t = std::make_shared<SrsTables>();
       t->device = c.device;
@@ -684,10 +710,13 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   auto t0 = clk::now();
   c.timing.resize(9, 0.0);
   for (int r = 0; r < 6; r++) c.timing[r] = 0.0;
+  Range range(ROUND_NAMES[0]);
   auto lap = [&](int r) {
     auto t1 = clk::now();
     c.timing[r] = std::chrono::duration<double, std::milli>(t1 - t0).count();
     t0 = t1;
+    if (r + 1 < 5) range.push(ROUND_NAMES[r + 1]);
+    else range.pop();
   };
   const bool gs = in.kind == KGS_GRANDSUM;
   const bool sel = in.sel_f != nullptr;
@@ -1023,61 +1052,6 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   c.reset_staging();
 }
 
-int fail(const KgsError& e) {
-  g_err = e.what();
-  return e.code;
-}
-
-// ------------------------------------------------------------------ ptau I/O
-struct PtauInfo {
-  int power = 0, ceremony = 0;
-  uint64_t s2_pos = 0, s2_size = 0, s3_pos = 0, s3_size = 0;
-};
-
-PtauInfo read_ptau_header(FILE* f, const char* path) {
-  PtauInfo info;
-  char magic[4];
-  uint32_t ver, nsec;
-  if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "ptau", 4) != 0)
-    throw KgsError(KGS_E_IO, std::string(path) + ": Invalid File format");
-  if (fread(&ver, 4, 1, f) != 1 || fread(&nsec, 4, 1, f) != 1) throw KgsError(KGS_E_IO, "truncated ptau");
-  if (ver > 1) throw KgsError(KGS_E_IO, std::string(path) + ": Invalid Version");
-  uint64_t pos = 12;
-  int nheaders = 0;
-  uint64_t s1_pos = 0, s1_size = 0;
-  for (uint32_t s = 0; s < nsec; s++) {
-    uint32_t id;
-    uint64_t size;
-    if (fseeko(f, (off_t)pos, SEEK_SET) || fread(&id, 4, 1, f) != 1 || fread(&size, 8, 1, f) != 1)
-      throw KgsError(KGS_E_IO, "truncated ptau section table");
-    pos += 12;
-    if (id == 1) {
-      nheaders++;
-      s1_pos = pos;
-      s1_size = size;
-    } else if (id == 2 && !info.s2_size) {
-      info.s2_pos = pos;
-      info.s2_size = size;
-    } else if (id == 3 && !info.s3_size) {
-      info.s3_pos = pos;
-      info.s3_size = size;
-    }
-    pos += size;
-  }
-  if (!nheaders) throw KgsError(KGS_E_IO, std::string(path) + ": File has no  header");
-  if (nheaders > 1) throw KgsError(KGS_E_IO, std::string(path) + ": File has more than one header");
-  uint32_t n8;
-  uint8_t q[32];
-  uint32_t pw[2];
-  if (fseeko(f, (off_t)s1_pos, SEEK_SET) || fread(&n8, 4, 1, f) != 1 || n8 != 32 || fread(q, 1, 32, f) != 32 ||
-      fread(pw, 4, 2, f) != 2)
-    throw KgsError(KGS_E_IO, std::string(path) + ": Invalid size");
-  if (memcmp(q, host::FQ_MOD.p, 32) != 0) throw KgsError(KGS_E_IO, "ptau curve is not bn128");
-  if (4 + 32 + 8 != s1_size) throw KgsError(KGS_E_IO, "Invalid PTau header size");
-  info.power = (int)pw[0];
-  info.ceremony = (int)pw[1];
-  return info;
-}
 
 // ------------------------------------------------------------------ host G2 (synthetic ptau): host_pairing.hpp
 using host::Fq2;
@@ -1109,8 +1083,6 @@ std::vector<uint8_t> g1_fixed_table() {
 // ================================================================== C-ABI
 extern "C" {
 
-const char* kgs_last_error(void) { return g_err.c_str(); }
-const char* kgs_version(void) { return "kgs-mi355x 0.1 (gfx950)"; }
 
 int kgs_ctx_create(int device, kgs_ctx_t** out) {
   try {
@@ -1129,9 +1101,9 @@ int kgs_ctx_create(int device, kgs_ctx_t** out) {
     *out = c;
     return KGS_OK;
   } catch (const KgsError& e) {
-    return fail(e);
+    return kgs_fail(e);
   } catch (const std::exception& e) {
-    g_err = e.what();
+    kgs_errbuf() = e.what();
     return KGS_E_HIP;
   }
 }
@@ -1147,10 +1119,10 @@ void kgs_ctx_destroy(kgs_ctx_t* ctx) {
 #define API_END                               \
   }                                           \
   catch (const KgsError& e) {                 \
-    return fail(e);                           \
+    return kgs_fail(e);                           \
   }                                           \
   catch (const std::exception& e) {           \
-    g_err = e.what();                         \
+    kgs_errbuf() = e.what();                         \
     return KGS_E_HIP;                         \
   }                                           \
   return KGS_OK;
@@ -1177,16 +1149,6 @@ int kgs_srs_load_points(kgs_ctx_t* ctx, const uint8_t* g1_lem, uint64_t npts, in
   API_END
 }
 
-int kgs_ptau_power(const char* path, int* power) {
-  API_BEGIN
-  if (!path || !power) throw KgsError(KGS_E_ARG, "NULL argument");
-  FILE* f = fopen(path, "rb");
-  if (!f) throw KgsError(KGS_E_IO, std::string("cannot open ") + path);
-  std::unique_ptr<FILE, int (*)(FILE*)> guard(f, fclose);
-  *power = read_ptau_header(f, path).power;
-  API_END
-}
-
 int kgs_srs_load_ptau(kgs_ctx_t* ctx, const char* path, int nbits_max) {
   API_BEGIN
   if (!ctx || !path) throw KgsError(KGS_E_ARG, "NULL argument");
@@ -1209,6 +1171,7 @@ int kgs_srs_load_ptau(kgs_ctx_t* ctx, const char* path, int nbits_max) {
   // grow-only: tables loaded for a larger domain of the same file serve every smaller proof
   if (ctx->srs && ctx->srs->file == file && ctx->srs->nbits_max >= nbits_max) return KGS_OK;
   uint64_t avail = info.s2_size / 64;
+  if (avail < 2) throw KgsError(KGS_E_IO, std::string(path) + ": ptau has no tauG1 section");
   uint64_t need = 1ull << (nbits_max + 1);
   if (need > avail) need = avail;
   std::vector<uint8_t> pts(need * 64);
@@ -1225,18 +1188,6 @@ int kgs_srs_info(kgs_ctx_t* ctx, int* power, uint64_t* npts, int* window_c) {
   if (power) *power = ctx->srs_power;
   if (npts) *npts = ctx->tb.npts;
   if (window_c) *window_c = ctx->tb.c;
-  API_END
-}
-
-int kgs_ptau_read_tau_g2(const char* path, uint8_t out128[128]) {
-  API_BEGIN
-  FILE* f = fopen(path, "rb");
-  if (!f) throw KgsError(KGS_E_IO, std::string("cannot open ") + path);
-  std::unique_ptr<FILE, int (*)(FILE*)> guard(f, fclose);
-  PtauInfo info = read_ptau_header(f, path);
-  if (info.s3_size < 256) throw KgsError(KGS_E_IO, "tauG2 section too small");
-  if (fseeko(f, (off_t)(info.s3_pos + 128), SEEK_SET) || fread(out128, 1, 128, f) != 128)
-    throw KgsError(KGS_E_IO, "cannot read [tau]_2");
   API_END
 }
 
@@ -1314,11 +1265,6 @@ int kgs_ptau_write_synthetic(kgs_ctx_t* ctx, const char* path, int power, const 
   API_END
 }
 
-int kgs_proof_shape(int kind, int npols, int selected, int* n_commitments, int* n_evaluations) {
-  if (n_commitments) *n_commitments = 2 * npols + (selected ? 2 : 0) + 4;
-  if (n_evaluations) *n_evaluations = (kind == KGS_GRANDSUM ? 2 : 1) * npols + (selected ? 2 : 0) + 1;
-  return KGS_OK;
-}
 
 namespace {
 // host copies between pageable caller buffers and the pinned staging area, split over threads
@@ -1389,7 +1335,9 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   }
   using hclk = std::chrono::steady_clock;
   const auto h0 = hclk::now();
+  Range rin("kgs.host.input_copy");
   par_copy(in_jobs);
+  rin.pop();
   const auto h1 = hclk::now();
   for (size_t v = 0; v < in_jobs.size(); v++)
     HC(hipMemcpyAsync(dsts[v], in_jobs[v].dst, E, hipMemcpyHostToDevice, ctx->st));
@@ -1420,7 +1368,9 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   const auto h2 = hclk::now();
   prove_impl(*ctx, in, commitments_out, evaluations_out);  // ends synchronised
   const auto h3 = hclk::now();
+  Range rout("kgs.host.writeback_wait");
   if (out_copy.t.joinable()) out_copy.t.join();
+  rout.pop();
   const auto h4 = hclk::now();
   // host-boundary phases: [6] input copy into pinned staging, [7] prover, [8] write-back wait
   ctx->timing.resize(9, 0.0);

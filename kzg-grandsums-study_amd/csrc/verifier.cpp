@@ -207,6 +207,13 @@ thread_local std::string v_err;
 
 extern "C" {
 
+int kgs_proof_shape(int kind, int npols, int selected, int* n_commitments, int* n_evaluations) {
+  if (npols < 1 || npols > (1 << 20)) return KGS_E_ARG;
+  if (n_commitments) *n_commitments = 2 * npols + (selected ? 2 : 0) + 4;
+  if (n_evaluations) *n_evaluations = (kind == KGS_GRANDSUM ? 2 : 1) * npols + (selected ? 2 : 0) + 1;
+  return KGS_OK;
+}
+
 int kgs_verify(int kind, int nbits, int npols, int selected, const uint8_t* commitments, const uint8_t* evaluations,
                const uint8_t tau_g2[128]) {
   if ((kind != KGS_GRANDSUM && kind != KGS_GRANDPRODUCT) || nbits < 1 || nbits > 28 || npols < 1 || !commitments ||
