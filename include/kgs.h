@@ -73,6 +73,33 @@ int kgs_shard_range(uint64_t n, int rank, int world, uint64_t* lo, uint64_t* hi)
  * X,Y,ZZ,ZZZ LE Montgomery Fq, ZZ == 0 is infinity): sum_k 2^k sum_r T_k^(r) -> affine LEM */
 int kgs_msm_combine(const uint8_t* T_all, int nparts, int c, uint8_t out_lem[64]);
 
+/* ---- multi-GPU: the distributed prover (north_star: "the MSM and NTT
+ * shard ... by scalar/point range and by butterfly stage across the 8 GPUs of one node").
+ * A context attached to a group of W ranks (W = 1, 2, 4, 8 or 16; one context per rank) proves with
+ * EVERY vector sharded: NTTs as a local transform + one all-to-all (CYCLIC <-> E layouts), the
+ * grand-sum/product builder as a local scan + one all-gather of rank totals, the quotient and the
+ * divisibility check on local slices with halo elements, Horner on CYCLIC slices, the synthetic
+ * divisions on BLOCK slices with one all-gather of carries, and every MSM over the rank's slice of
+ * the SRS. Each rank passes the FULL inputs (as for kgs_prove / kgs_prove_device) and receives the
+ * identical, full proof (byte-identical to the single-GPU prover). Needs n >= 2 W^2.
+ * All ranks must call the prover with the same arguments, in the same order.
+ * Transports:
+ *   local : several contexts of ONE process (one host thread per rank; devices may differ)
+ *   host  : any host all-gather callback (e.g. torch.distributed gloo); device data via the host
+ *   rccl  : one process per GPU, RCCL over xGMI (rank 0 makes the id, the caller broadcasts it)
+ * A rank failing with anything but a semantic prover error (not well calculated / not divisible /
+ * does not divide / bad argument) aborts the group: the other ranks fail too, the group is spent. */
+typedef struct kgs_group kgs_group_t;
+int kgs_group_create_local(int world, kgs_group_t** out);
+int kgs_group_create_host(int world, kgs_allgather_fn fn, void* user, kgs_group_t** out);
+int kgs_group_rccl_unique_id(uint8_t id[128]);
+int kgs_group_create_rccl(int rank, int world, const uint8_t id[128], int device, kgs_group_t** out);
+void kgs_group_destroy(kgs_group_t* g);
+int kgs_group_world(kgs_group_t* g, int* world);
+/* attach (g != NULL) or detach (g == NULL) the distributed prover for this rank; a world-1 group
+ * runs the distributed code path on one rank (exercises a transport end to end on one GPU) */
+int kgs_ctx_set_group(kgs_ctx_t* ctx, kgs_group_t* g, int rank);
+
 /* MSM lanes per context (default 2): with 2, the independent commitments of one prover round
  * (round 1's F_i / T_i, round 5's W_xi / W_xiw) alternate between two HIP streams with separate
  * work buffers, so one MSM's latency-bound tail overlaps the other's bucket accumulation

@@ -87,6 +87,16 @@ def lib():
         L.kgs_shard_range.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_uint64)]
         L.kgs_msm_combine.argtypes = [c_u8p, ctypes.c_int, ctypes.c_int, c_u8p]
+        L.kgs_group_create_local.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.kgs_group_create_host.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.POINTER(ctypes.c_void_p)]
+        L.kgs_group_rccl_unique_id.argtypes = [c_u8p]
+        L.kgs_group_create_rccl.argtypes = [ctypes.c_int, ctypes.c_int, c_u8p, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_void_p)]
+        L.kgs_group_destroy.argtypes = [ctypes.c_void_p]
+        L.kgs_group_destroy.restype = None
+        L.kgs_group_world.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        L.kgs_ctx_set_group.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -186,6 +196,69 @@ def torch_allgather(group=None, device=None):
     return fn
 
 
+class Group:
+    """Rank group of the distributed prover (kgs_group_t; Context.set_group): every vector of a
+    proof sharded over `world` ranks, one context per rank.
+      Group.local(world)                 several contexts of this process (one host thread per rank)
+      Group.host(world, allgather)       any host all-gather(bytes) -> world * bytes (e.g. gloo);
+                                         device data is staged through the host
+      Group.rccl(rank, world, id, dev)   one process per GPU, RCCL over xGMI; id = rccl_unique_id()
+                                         made on rank 0 and broadcast by the caller"""
+
+    def __init__(self, handle, world, keep=None):
+        self._h = handle
+        self.world = world
+        self._keep = keep
+
+    @classmethod
+    def local(cls, world):
+        h = ctypes.c_void_p()
+        _check(lib().kgs_group_create_local(world, ctypes.byref(h)))
+        return cls(h, world)
+
+    @classmethod
+    def host(cls, world, allgather):
+        def _cb(user, send, recv, nbytes):
+            try:
+                out = allgather(ctypes.string_at(send, nbytes))
+                if len(out) != nbytes * world:
+                    return -1
+                ctypes.memmove(recv, out, len(out))
+                return 0
+            except Exception:  # reported to the caller as KGS_E_COMM
+                import traceback
+                traceback.print_exc()
+                return -1
+        cb = ALLGATHER_FN(_cb)
+        h = ctypes.c_void_p()
+        _check(lib().kgs_group_create_host(world, ctypes.cast(cb, ctypes.c_void_p), None, ctypes.byref(h)))
+        return cls(h, world, cb)
+
+    @classmethod
+    def rccl(cls, rank, world, uid, device):
+        h = ctypes.c_void_p()
+        _check(lib().kgs_group_create_rccl(rank, world, _buf(uid), device, ctypes.byref(h)))
+        return cls(h, world)
+
+    def close(self):
+        if self._h:
+            lib().kgs_group_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def rccl_unique_id():
+    """128-byte RCCL communicator id (kgs_group_rccl_unique_id), made on rank 0 and broadcast."""
+    out = ctypes.create_string_buffer(128)
+    _check(lib().kgs_group_rccl_unique_id(out))
+    return out.raw
+
+
 class ThreadGroup:
     """In-process all-gather between `world` contexts driven by `world` host threads (one rank
     each): several GPUs of one process, or the sharded path rehearsed on a single GPU."""
@@ -275,6 +348,12 @@ class Context:
         self._shard_cb = ALLGATHER_FN(_cb) if world > 1 else None
         fp = ctypes.cast(self._shard_cb, ctypes.c_void_p) if world > 1 else None
         _check(lib().kgs_ctx_set_shard(self._h, rank, world, fp, None))
+
+    def set_group(self, group, rank=0):
+        """Attach the distributed prover (kgs_ctx_set_group): this context is `rank` of `group`;
+        None detaches. Keeps the group alive while attached."""
+        _check(lib().kgs_ctx_set_group(self._h, group._h if group is not None else None, rank))
+        self._group = group
 
     def load_ptau(self, path, nbits_max=-1):
         _check(lib().kgs_srs_load_ptau(self._h, os.fsencode(path), nbits_max))

@@ -74,7 +74,8 @@ void launch_quotient(hipStream_t st, bool prod, bool sel, uint32_t* q, const uin
                      const uint32_t* T, const uint32_t* SF, const uint32_t* ST, const uint32_t* inv_nxm1,
                      const uint32_t* scalars, int lcs, uint32_t rot);
 void launch_divcheck(hipStream_t st, bool prod, bool sel, uint32_t* flag, const uint32_t* S, const uint32_t* f,
-                     const uint32_t* t, const uint32_t* sf, const uint32_t* stt, const uint32_t* scalars, uint64_t n);
+                     const uint32_t* t, const uint32_t* sf, const uint32_t* stt, const uint32_t* scalars, uint64_t n,
+                     const uint32_t* S_next = nullptr, uint64_t gbase = 0);
 void launch_eval_tiles(hipStream_t st, uint32_t* part, const EvalBatch& eb, const uint32_t* xp, uint32_t ntiles_max);
 void launch_divide(hipStream_t st, uint32_t* q, uint32_t* flag, const uint32_t* a, uint64_t L, const uint32_t* xp,
                    uint32_t* part, uint32_t* carry);
@@ -83,11 +84,29 @@ void launch_nxm1(hipStream_t st, uint32_t* out, const uint32_t* tw, uint64_t hal
                  const uint32_t* np, int lcs, uint64_t wstride);
 constexpr uint64_t EVAL_TILE = 2048;
 
+// dist.hip (the distributed prover's rank-local kernels; layouts in prover_dist.cpp)
+void launch_gather_e(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t N, int W, int r, bool to_mont);
+void launch_dfwd_pack(hipStream_t st, uint32_t* send, const uint32_t* Z, int logMl, int W, int r, const uint32_t* tw,
+                      int logN);
+void launch_dfwd_wdft(hipStream_t st, uint32_t* out, const uint32_t* recv, int logMl, int W, const uint32_t* tw, int logN);
+void launch_dinv_wdft_pack(hipStream_t st, uint32_t* send, const uint32_t* loc, int logMl, int W, int r,
+                           const uint32_t* tw_inv, int logN);
+void launch_unpack_c2b(hipStream_t st, uint32_t* out, const uint32_t* recv, uint64_t Lb, int W);
+void launch_scan_fix(hipStream_t st, bool prod, uint32_t* out, const uint32_t* off, uint64_t n);
+void launch_e_heads(hipStream_t st, uint32_t* heads, const uint32_t* S, uint64_t Ml, int W, int rot);
+void launch_quotient_e(hipStream_t st, bool prod, bool sel, uint32_t* q, const uint32_t* S, const uint32_t* F,
+                       const uint32_t* T, const uint32_t* SF, const uint32_t* ST, const uint32_t* nxm1,
+                       const uint32_t* scalars, const uint32_t* halo, uint64_t Ml, int W, int r, int rot);
+void launch_nxm1_e(hipStream_t st, uint32_t* out, const uint32_t* tw, int lcs, const uint32_t* gp, const uint32_t* np,
+                   int W, int r);
+void launch_div_fix(hipStream_t st, uint32_t* q, const uint32_t* pz, const uint32_t* c, uint64_t Lb);
+
 // msm.hip
 void msm_build_table(hipStream_t st, uint32_t* table, uint64_t npts, int c, int W, uint32_t* tmp_xyzz,
                      uint32_t* scratch);
+// scalars[i] multiplies SRS point pbase + pstride * i (pbase + pstride * (N - 1) < tb.npts)
 void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* scalars, uint64_t N, uint32_t* T_out,
-             hipEvent_t* ev = nullptr);
+             hipEvent_t* ev = nullptr, uint64_t pbase = 0, uint64_t pstride = 1);
 void launch_fixed_base(hipStream_t st, uint32_t* out_xyzz, const uint32_t* sc, uint64_t count, const uint32_t* tbl);
 void launch_batch_affine(hipStream_t st, uint32_t* out_aff, const uint32_t* in_xyzz, uint32_t* scratch, uint64_t npts);
 

@@ -217,11 +217,13 @@ __global__ void __launch_bounds__(64) k_sort_scan(uint32_t* __restrict__ hi_off,
 }
 
 // dynamic LDS: 256 * W * (4 + 2) bytes of staging
+// scalar i multiplies SRS point pbase + pstride * i (a contiguous or strided slice of the SRS)
 template <int C>
 __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, uint8_t* __restrict__ tlo,
                                                    const uint32_t* __restrict__ bh, const uint32_t* __restrict__ ptot,
                                                    const uint32_t* __restrict__ hi_off, const uint32_t* __restrict__ sc,
-                                                   uint64_t N, uint64_t Nsrs, int lob, int NH, uint32_t nblk) {
+                                                   uint64_t N, uint64_t Nsrs, uint64_t pbase, uint64_t pstride, int lob,
+                                                   int NH, uint32_t nblk) {
   KGS_AUX_PRIO();
   constexpr int W = (255 + C - 1) / C;
   extern __shared__ uint32_t smem[];
@@ -254,7 +256,7 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
         if (!d[j]) continue;
         const uint32_t k = (uint32_t)(d[j] < 0 ? -d[j] : d[j]);
         const uint32_t pos = atomicAdd(&cur[part_of(k, lob)], 1u);
-        sval[pos] = (uint32_t)((uint64_t)j * Nsrs + i) | (d[j] < 0 ? 0x80000000u : 0u);
+        sval[pos] = (uint32_t)((uint64_t)j * Nsrs + pbase + pstride * i) | (d[j] < 0 ? 0x80000000u : 0u);
         skey[pos] = (uint16_t)(k - 1);
       }
     }
@@ -611,7 +613,7 @@ __global__ void __launch_bounds__(128) k_bitsum_rc(uint32_t* __restrict__ T, con
 
 // ------------------------------------------------------------------ driver (device part)
 void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* scalars, uint64_t N,
-             uint32_t* T_out, hipEvent_t* ev) {
+             uint32_t* T_out, hipEvent_t* ev, uint64_t pbase, uint64_t pstride) {
   // ev (optional, 5 events): [0] start, [1] after digits+sort, [2] after k_accumulate,
   // [3] after combine, [4] after bit-sum reduction
   if (ev) hipEventRecord(ev[0], st);
@@ -634,7 +636,7 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
     hipLaunchKernelGGL(k_sort_scan_blocks, dim3(NH), dim3(256), 0, st, bh, ptot, nblk);                       \
     hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(64), 0, st, hi_off, ptot, NH, w.offsets, B);               \
     hipLaunchKernelGGL(k_sort_part<CC>, dim3(nblk), dim3(256), part_lds, st, (uint32_t*)w.digit, w.lo, bh,   \
-                       ptot, hi_off, scalars, N, tb.npts, lob, NH, nblk);                                     \
+                       ptot, hi_off, scalars, N, tb.npts, pbase, pstride, lob, NH, nblk);                     \
     break;
     KGS_SORT_C(7) KGS_SORT_C(8) KGS_SORT_C(9) KGS_SORT_C(10) KGS_SORT_C(11) KGS_SORT_C(12)
     KGS_SORT_C(13) KGS_SORT_C(14) KGS_SORT_C(15) KGS_SORT_C(16) KGS_SORT_C(17)

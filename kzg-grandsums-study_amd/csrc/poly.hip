@@ -10,6 +10,7 @@
 // Every kernel is integer arithmetic on 32 B Montgomery elements; most are VALU bound (one or
 // more 254-bit Montgomery products per element), the rest HBM bound.
 #include "kernels.hpp"
+#include "poly_math.hpp"
 
 namespace kgs {
 
@@ -371,36 +372,10 @@ __global__ void __launch_bounds__(256) k_quotient(uint32_t* __restrict__ q, cons
   const uint32_t j = (i + rot) & (uint32_t)(cs - 1);
   const uint32_t pj = brev(j, lcs);
   const fr s = fr::load(S + 8 * p), sw = fr::load(S + 8 * (uint64_t)pj);
-  const fr fg = fr::load(F + 8 * p) + gamma, tg = fr::load(T + 8 * p) + gamma;
-  fr acc = fr::zero();
-  fr sf, st;
-  if (SEL) {
-    sf = fr::load(SF + 8 * p);
-    st = fr::load(ST + 8 * p);
-    // alpha^3 (selT - selT^2) + alpha^2 (selF - selF^2)  ==  ((selT-selT^2)*alpha + (selF-selF^2))*alpha^2
-    acc = (st - st.sqr()) * alpha + (sf - sf.sqr());
-    acc = acc * alpha;  // will be multiplied by alpha once more below together with Q1
-  }
-  fr q1;
-  if (!PROD) {
-    q1 = (sw - s) * fg * tg;
-    if (SEL) q1 = q1 + st * fg - sf * tg;
-    else q1 = q1 + (fg - tg);  // F - T
-  } else {
-    const fr one = fr::one();
-    fr dT = tg, dF = fg;
-    if (SEL) {
-      dT = st * (tg - one) + one;
-      dF = sf * (fg - one) + one;
-    }
-    q1 = sw * dT - s * dF;
-  }
-  acc = (acc + q1) * alpha;
+  const fr sf = SEL ? fr::load(SF + 8 * p) : fr::zero(), st = SEL ? fr::load(ST + 8 * p) : fr::zero();
+  fr acc = quotient_core<PROD, SEL>(s, sw, fr::load(F + 8 * p), fr::load(T + 8 * p), sf, st, alpha, gamma);
   const fr zinv = (rot == 2 && (i & 1)) ? z1 : z0;
-  acc = acc * zinv;
-  // + L1(x) * S(x) / Z_H(x) = S(x) / (n (x-1))   (grand-product: (Z(x) - 1))
-  fr l = PROD ? (s - fr::one()) : s;
-  acc = acc + l * fr::load(inv_nxm1 + 8 * p);
+  acc = acc * zinv + quotient_l1<PROD>(s, fr::load(inv_nxm1 + 8 * p));
   acc.store(q + 8 * p);
 }
 
@@ -419,45 +394,29 @@ void launch_quotient(hipStream_t st, bool prod, bool sel, uint32_t* q, const uin
 }
 
 // Divisibility of the quotient numerator by Z_H, evaluated on H (natural order): N(w^i) == 0.
+// S_next: S at the natural index following the last one of this array (the wrap S[0] on one GPU,
+// the next rank's first element when H is BLOCK-distributed); gbase: natural index of element 0.
 template <bool PROD, bool SEL>
 __global__ void k_divcheck(uint32_t* __restrict__ flag, const uint32_t* __restrict__ S, const uint32_t* __restrict__ f,
                            const uint32_t* __restrict__ t, const uint32_t* __restrict__ sfp, const uint32_t* __restrict__ stp,
-                           const uint32_t* __restrict__ sc, uint64_t n) {
+                           const uint32_t* __restrict__ sc, uint64_t n, const uint32_t* __restrict__ S_next,
+                           uint64_t gbase) {
   KGS_AUX_PRIO();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const fr alpha = fr::load(sc), gamma = fr::load(sc + 8);
-  const uint64_t j = i + 1 == n ? 0 : i + 1;
-  const fr s = fr::load(S + 8 * i), sw = fr::load(S + 8 * j);
-  const fr fg = fr::load(f + 8 * i) + gamma, tg = fr::load(t + 8 * i) + gamma;
-  fr acc = fr::zero(), sf, st;
-  if (SEL) {
-    sf = fr::load(sfp + 8 * i);
-    st = fr::load(stp + 8 * i);
-    acc = ((st - st.sqr()) * alpha + (sf - sf.sqr())) * alpha;
-  }
-  fr q1;
-  if (!PROD) {
-    q1 = (sw - s) * fg * tg;
-    if (SEL) q1 = q1 + st * fg - sf * tg;
-    else q1 = q1 + (fg - tg);
-  } else {
-    const fr one = fr::one();
-    fr dT = tg, dF = fg;
-    if (SEL) {
-      dT = st * (tg - one) + one;
-      dF = sf * (fg - one) + one;
-    }
-    q1 = sw * dT - s * dF;
-  }
-  acc = (acc + q1) * alpha;
-  if (i == 0) acc = acc + (PROD ? s - fr::one() : s);  // L1(w^0) = 1
+  const fr s = fr::load(S + 8 * i), sw = i + 1 == n ? fr::load(S_next) : fr::load(S + 8 * (i + 1));
+  const fr sf = SEL ? fr::load(sfp + 8 * i) : fr::zero(), st = SEL ? fr::load(stp + 8 * i) : fr::zero();
+  fr acc = quotient_core<PROD, SEL>(s, sw, fr::load(f + 8 * i), fr::load(t + 8 * i), sf, st, alpha, gamma);
+  if (gbase + i == 0) acc = acc + (PROD ? s - fr::one() : s);  // L1(w^0) = 1
   if (!acc.is_zero()) atomicOr(flag, 1u);
 }
 
 void launch_divcheck(hipStream_t st, bool prod, bool sel, uint32_t* flag, const uint32_t* S, const uint32_t* f,
-                     const uint32_t* t, const uint32_t* sf, const uint32_t* stt, const uint32_t* scalars, uint64_t n) {
-#define KGS_D(P, S_) hipLaunchKernelGGL((k_divcheck<P, S_>), dim3(nb(n)), dim3(256), 0, st, flag, S, f, t, sf, stt, scalars, n);
+                     const uint32_t* t, const uint32_t* sf, const uint32_t* stt, const uint32_t* scalars, uint64_t n,
+                     const uint32_t* S_next, uint64_t gbase) {
+  if (!S_next) S_next = S;
+#define KGS_D(P, S_) hipLaunchKernelGGL((k_divcheck<P, S_>), dim3(nb(n)), dim3(256), 0, st, flag, S, f, t, sf, stt, scalars, n, S_next, gbase);
   if (prod) {
     if (sel) { KGS_D(true, true) } else { KGS_D(true, false) }
   } else {

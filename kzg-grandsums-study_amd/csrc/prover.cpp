@@ -41,50 +41,14 @@
 #include "ptau_io.hpp"
 #include "transcript.hpp"
 
+#include "context.hpp"
+
 using namespace kgs;
+using namespace kgsi;
 using host::Fq;
 using host::Fr;
 
-namespace {
-
-#define HC(x)                                                                                    \
-  do {                                                                                           \
-    hipError_t e_ = (x);                                                                         \
-    if (e_ != hipSuccess)                                                                        \
-      throw KgsError(KGS_E_HIP, std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x); \
-  } while (0)
-
-static void check_launch() {
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) throw KgsError(KGS_E_HIP, std::string("HIP launch error: ") + hipGetErrorString(e));
-}
-
-using host::fr_w;
-
-// roctx ranges (rocprofv3 --marker-trace): one per prover round and per host-boundary phase, so a
-// trace shows where a proof's host wall time goes next to its kernels. -DKGS_NO_ROCTX removes them.
-struct Range {
-  bool open = false;
-  explicit Range(const char* name = nullptr) {
-    if (name) push(name);
-  }
-  void push(const char* name) {
-    pop();
-#ifndef KGS_NO_ROCTX
-    roctxRangePushA(name);
-#endif
-    open = true;
-  }
-  void pop() {
-#ifndef KGS_NO_ROCTX
-    if (open) roctxRangePop();
-#endif
-    open = false;
-  }
-  ~Range() { pop(); }
-};
-const char* const ROUND_NAMES[5] = {"kgs.round1.commit_witness", "kgs.round2.grand_poly", "kgs.round3.quotient",
-                                    "kgs.round4.evaluations", "kgs.round5.openings"};
+namespace kgsi {
 
 // Every device allocation goes through here. KGS_DEBUG_ALLOC_LIMIT=<bytes> (fault injection for the
 // tests) makes any single request above that size fail as out-of-memory.
@@ -99,208 +63,13 @@ hipError_t dev_malloc(void** p, size_t bytes) {
   return hipMalloc(p, bytes);
 }
 
-// multisets per proof (the reference has no limit; this only bounds host-side bookkeeping)
-constexpr int KGS_MAX_POLS = 1024;
-
-#ifndef KGS_C_MAX
-#define KGS_C_MAX 17
-#endif
-
-struct DBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-};
-
-// Read-only device tables shared by every context on a device (one copy per device, not per
-// in-flight context): the SRS window tables of a ptau (keyed by file identity and the domain they
-// were loaded for) and the NTT / coset twiddle tables (the largest domain built so far serves every
-// smaller one: stage tables tw[h + t] = w_2h^t do not depend on the maximum domain). Published only
-// after their build has completed (stream synchronised), released when the last context drops them.
-struct SrsTables {
-  int device = 0;
-  std::string file;  // file identity (path + size + mtime) or "mem#<id>"
-  int power = -1, nbits_max = -1;
-  MsmTables tb;
-  ~SrsTables() {
-    if (tb.table) {
-      hipSetDevice(device);
-      hipFree(tb.table);
-    }
-  }
-};
-
-struct DomainTables {
-  int device = 0, logM = -1;
-  uint32_t* mem = nullptr;
-  uint32_t *tw_fwd = nullptr, *tw_inv = nullptr, *coset_pow = nullptr, *coset_ipow = nullptr, *invm = nullptr;
-  ~DomainTables() {
-    if (mem) {
-      hipSetDevice(device);
-      hipFree(mem);
-    }
-  }
-};
-
-std::mutex g_reg_mu;  // lock order: kgs_ctx::mu, then g_reg_mu
+std::mutex g_reg_mu;
 std::vector<std::weak_ptr<SrsTables>> g_srs_reg;
 std::vector<std::weak_ptr<DomainTables>> g_dom_reg;
 
-}  // namespace
+}  // namespace kgsi
 
-struct kgs_ctx {
-  // every C-ABI entry point that touches the context holds mu: a busy context blocks its caller,
-  // it is never entered twice (the JS backend runs prove() calls on libuv worker threads)
-  std::mutex mu;
-  int device = 0;
-  hipStream_t st = nullptr;
-  std::map<std::string, DBuf> pool;
-  // pinned staging of the host-buffer boundary (kgs_prove's inputs and Montgomery write-back)
-  uint8_t* h_io = nullptr;
-  size_t h_io_bytes = 0;
-  // pinned staging
-  uint8_t* h_pin = nullptr;
-  size_t h_pin_bytes = 0;
-  size_t h_pin_off = 0;
-  uint32_t* d_scal = nullptr;  // device scalar area
-  size_t d_scal_off = 0;
-  static constexpr size_t SCAL_BYTES = 1 << 16;
-  // SRS (shared, read-only) and this context's views of it
-  std::shared_ptr<SrsTables> srs;
-  int srs_power = -1;
-  int nbits_max = -1;
-  MsmTables tb;
-  MsmWork mw;
-  uint64_t work_npts = 0;  // MSM work buffers (both lanes) are sized for this many points
-  int msm_slots = 0;       // commitments in flight per proof (msm_T slots)
-  // second MSM lane: independent commitments of one round (R1's F_i/T_i, R5's two W) alternate
-  // between st and st2 (own work buffers), so one MSM's latency-bound tail overlaps the other's
-  // bucket accumulation
-  hipStream_t st2 = nullptr;
-  hipStream_t st_copy = nullptr;  // Montgomery write-back of the host-buffer boundary
-  hipEvent_t ev_fork = nullptr, ev_copy = nullptr;
-  MsmWork mw2;
-  int msm_lanes = 2;  // kgs_ctx_set_msm_lanes
-  uint64_t msm_nseg_max = 0;
-  // domain tables (M = 2^logM; shared) and this context's views of them
-  std::shared_ptr<DomainTables> dom;
-  int logM = -1;
-  uint32_t *tw_fwd = nullptr, *tw_inv = nullptr, *coset_pow = nullptr, *coset_ipow = nullptr, *invm = nullptr;
-  std::map<std::pair<int, int>, uint32_t*> nxm1;  // (nbits, lcs) -> 1/(n(x-1)) on the coset (bitrev)
-  std::vector<double> timing;
-  // MSM point-range sharding (kgs_ctx_set_shard): world > 1 splits every commitment MSM
-  int shard_rank = 0, shard_world = 1;
-  kgs_allgather_fn shard_fn = nullptr;
-  void* shard_user = nullptr;
-
-  ~kgs_ctx() {
-    hipSetDevice(device);
-    // every stream may still read pool buffers or pinned staging: drain all before freeing
-    if (st) hipStreamSynchronize(st);
-    if (st2) hipStreamSynchronize(st2);
-    if (st_copy) hipStreamSynchronize(st_copy);
-    for (auto& kv : pool) hipFree(kv.second.p);
-    if (h_pin) hipHostFree(h_pin);
-    if (h_io) hipHostFree(h_io);
-    if (ev_fork) hipEventDestroy(ev_fork);
-    if (ev_copy) hipEventDestroy(ev_copy);
-    if (st_copy) hipStreamDestroy(st_copy);
-    if (st2) hipStreamDestroy(st2);
-    if (st) hipStreamDestroy(st);
-    {
-      std::lock_guard<std::mutex> lk(g_reg_mu);  // shared tables are released under the registry lock
-      srs.reset();
-      dom.reset();
-    }
-  }
-
-  // A failed (re)allocation leaves the slot empty (bytes = 0), never a stale size over a freed block.
-  uint32_t* buf(const std::string& name, size_t bytes) {
-    DBuf& b = pool[name];
-    if (b.bytes < bytes) {
-      if (b.p) {
-        sync();  // any stream may still use the old block
-        HC(hipFree(b.p));
-        b.p = nullptr;
-        b.bytes = 0;
-      }
-      const size_t sz = bytes < 64 ? 64 : bytes;
-      HC(dev_malloc(&b.p, sz));
-      b.bytes = sz;
-    }
-    return (uint32_t*)b.p;
-  }
-  uint8_t* io(size_t bytes) {
-    if (h_io_bytes < bytes) {
-      if (h_io) {
-        sync();
-        HC(hipHostFree(h_io));
-        h_io = nullptr;
-        h_io_bytes = 0;
-      }
-      HC(hipHostMalloc((void**)&h_io, bytes, hipHostMallocDefault));
-      h_io_bytes = bytes;
-    }
-    return h_io;
-  }
-  void ensure_pin(size_t bytes) {
-    if (h_pin_bytes >= bytes) return;
-    if (h_pin) {
-      sync();
-      HC(hipHostFree(h_pin));
-      h_pin = nullptr;
-      h_pin_bytes = 0;
-      h_pin_off = 0;
-    }
-    HC(hipHostMalloc((void**)&h_pin, bytes, hipHostMallocDefault));
-    h_pin_bytes = bytes;
-  }
-  // bump-allocated pinned region (valid until reset_staging(), i.e. until the next sync point)
-  uint8_t* pin(size_t bytes) {
-    bytes = (bytes + 63) & ~size_t(63);
-    if (h_pin_off + bytes > h_pin_bytes) throw KgsError(KGS_E_ARG, "pinned staging exhausted");
-    uint8_t* p = h_pin + h_pin_off;
-    h_pin_off += bytes;
-    return p;
-  }
-  // copy host scalars to the device scalar area; returns the device pointer
-  uint32_t* scal(const Fr* v, int count) {
-    size_t bytes = 32 * (size_t)count;
-    if (d_scal_off + bytes > SCAL_BYTES) throw KgsError(KGS_E_ARG, "scalar staging exhausted");
-    uint8_t* h = pin(bytes);
-    for (int i = 0; i < count; i++) v[i].to_bytes(h + 32 * i);
-    uint32_t* d = d_scal + d_scal_off / 4;
-    d_scal_off += bytes;
-    HC(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
-    return d;
-  }
-  void sync() {
-    HC(hipStreamSynchronize(st));
-    if (st2) HC(hipStreamSynchronize(st2));
-    if (st_copy) HC(hipStreamSynchronize(st_copy));
-  }
-  void reset_staging() {
-    sync();
-    h_pin_off = 0;
-    d_scal_off = 0;
-  }
-  void use_srs(const std::shared_ptr<SrsTables>& s) {
-    srs = s;
-    tb = s ? s->tb : MsmTables{};
-    srs_power = s ? s->power : -1;
-    nbits_max = s ? s->nbits_max : -1;
-  }
-  void use_domain(const std::shared_ptr<DomainTables>& d) {
-    dom = d;
-    logM = d->logM;
-    tw_fwd = d->tw_fwd;
-    tw_inv = d->tw_inv;
-    coset_pow = d->coset_pow;
-    coset_ipow = d->coset_ipow;
-    invm = d->invm;
-  }
-};
-
-namespace {
+namespace kgsi {
 
 // ------------------------------------------------------------------ domain tables
 // Shared per device: a context asking for 2^logM reuses any published table of at least that size.
@@ -512,10 +281,6 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
 // Polynomial.multiExponentiation (polynomial.js:1106-1115): device Pippenger -> c bit-sum points
 // T_k (XYZZ) -> host sum_k 2^k T_k -> affine LEM. Sharded (world > 1): this rank's point range
 // only; the partials of all ranks are all-gathered once per batch of commits (one prover round).
-struct Commit {
-  uint8_t* h_T = nullptr;  // pinned, c x 128 B (this rank's partial)
-  uint64_t N = 0;
-};
 
 void shard_range(uint64_t n, int rank, int world, uint64_t& lo, uint64_t& hi) {
   lo = (uint64_t)((unsigned __int128)n * (unsigned)rank / (unsigned)world);
@@ -533,28 +298,34 @@ void fork_lanes(kgs_ctx& c) {
   HC(hipStreamWaitEvent(c.st2, c.ev_fork, 0));
 }
 
-Commit commit_launch(kgs_ctx& c, const uint32_t* scalars, uint64_t N, int slot, int lane = 0) {
+Commit commit_launch_slice(kgs_ctx& c, const uint32_t* scalars, uint64_t count, uint64_t pbase, uint64_t pstride,
+                           uint64_t N, int slot, int lane) {
   Commit cm;
   cm.N = N;
   const int cc = c.tb.c;
   const int slots = c.msm_slots > 64 ? c.msm_slots : 64;
   if (slot >= slots) throw KgsError(KGS_E_ARG, "too many commitments in flight");
-  if (N > c.tb.npts) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
+  if (N > c.tb.npts || (count && pbase + pstride * (count - 1) >= c.tb.npts))
+    throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
   uint32_t* dT = c.buf("msm_T", (size_t)slots * cc * 128) + (size_t)slot * cc * 32;
   cm.h_T = c.pin((size_t)cc * 128);
-  uint64_t lo = 0, hi = N;
-  if (c.shard_world > 1) shard_range(N, c.shard_rank, c.shard_world, lo, hi);
-  if (hi == lo) {
+  if (count == 0) {
     memset(cm.h_T, 0, (size_t)cc * 128);  // ZZ == 0: infinity
     return cm;
   }
-  MsmTables tb = c.tb;
-  tb.table += (size_t)16 * lo;  // same window stride (npts), points [lo, hi)
   if (c.msm_lanes < 2) lane = 0;
   hipStream_t st = lane ? c.st2 : c.st;  // lane 1 was forked (fork_lanes) after the round's inputs
-  msm_run(st, tb, lane ? c.mw2 : c.mw, scalars + (size_t)8 * lo, hi - lo, dT);
+  msm_run(st, c.tb, lane ? c.mw2 : c.mw, scalars, count, dT, nullptr, pbase, pstride);
   check_launch();
   HC(hipMemcpyAsync(cm.h_T, dT, (size_t)cc * 128, hipMemcpyDeviceToHost, st));
+  return cm;
+}
+
+// MSM point-range sharding (kgs_ctx_set_shard): this rank's contiguous range of the N points
+Commit commit_launch(kgs_ctx& c, const uint32_t* scalars, uint64_t N, int slot, int lane) {
+  uint64_t lo = 0, hi = N;
+  if (c.shard_world > 1) shard_range(N, c.shard_rank, c.shard_world, lo, hi);
+  Commit cm = commit_launch_slice(c, scalars + (size_t)8 * lo, hi - lo, lo, 1, N, slot, lane);
   return cm;
 }
 
@@ -568,11 +339,12 @@ void combine_partials(const uint8_t* T_all, size_t part_stride, int nparts, int 
   acc.to_affine_lem(out);
 }
 
-// after sync: finish a batch of commits (one all-gather per batch when sharded)
-void commits_finish(kgs_ctx& c, const std::vector<Commit>& cms, std::vector<uint8_t*> outs) {
+// after sync: finish a batch of commits; with world > 1 the partials of all ranks are exchanged in
+// ONE all-gather per batch (one prover round) and summed on the host
+void commits_finish_with(kgs_ctx& c, const std::vector<Commit>& cms, std::vector<uint8_t*> outs, int world,
+                         const HostAllgather& ag) {
   const int cc = c.tb.c;
   const size_t tb = (size_t)cc * 128;
-  const int world = c.shard_world;
   bool any = false;
   for (auto& cm : cms) any |= cm.N > 0;
   if (world == 1 || !any) {
@@ -585,26 +357,25 @@ void commits_finish(kgs_ctx& c, const std::vector<Commit>& cms, std::vector<uint
   const size_t bytes = tb * cms.size();
   std::vector<uint8_t> send(bytes), recv(bytes * world);
   for (size_t i = 0; i < cms.size(); i++) memcpy(send.data() + i * tb, cms[i].h_T, tb);
-  if (!c.shard_fn) throw KgsError(KGS_E_COMM, "sharding enabled without an all-gather callback");
-  if (c.shard_fn(c.shard_user, send.data(), recv.data(), bytes) != 0)
-    throw KgsError(KGS_E_COMM, "shard all-gather failed");
+  ag(send.data(), recv.data(), bytes);
   for (size_t i = 0; i < cms.size(); i++) {
     if (cms[i].N) combine_partials(recv.data() + i * tb, bytes, world, cc, outs[i]);
     else host::G1::inf().to_affine_lem(outs[i]);
   }
 }
 
+void commits_finish(kgs_ctx& c, const std::vector<Commit>& cms, std::vector<uint8_t*> outs) {
+  commits_finish_with(c, cms, outs, c.shard_world, [&](const void* send, void* recv, size_t bytes) {
+    if (!c.shard_fn) throw KgsError(KGS_E_COMM, "sharding enabled without an all-gather callback");
+    if (c.shard_fn(c.shard_user, (const uint8_t*)send, (uint8_t*)recv, bytes) != 0)
+      throw KgsError(KGS_E_COMM, "shard all-gather failed");
+  });
+}
+
 void commit_finish(kgs_ctx& c, const Commit& cm, uint8_t out[64]) { commits_finish(c, {cm}, {out}); }
 
 // ------------------------------------------------------------------ Horner evaluation
 // returns p_j(x) for each poly of the batch
-struct EvalJob {
-  std::vector<const uint32_t*> src;
-  std::vector<uint64_t> len;
-  uint8_t* h_part = nullptr;
-  uint32_t ntiles = 0;
-  Fr x;
-};
 
 uint32_t* xpowers(kgs_ctx& c, const Fr& x) {
   Fr p[10];
@@ -658,28 +429,7 @@ std::vector<Fr> eval_finish(const EvalJob& j) {
 }
 
 // ------------------------------------------------------------------ the prover
-struct ProveIn {
-  int kind, nbits, npols;
-  std::vector<const uint32_t*> f_std, t_std;  // device, standard form
-  const uint32_t *sel_f = nullptr, *sel_t = nullptr;  // device, Montgomery (nullptr: unselected)
-  std::vector<uint8_t*> mont_f_out, mont_t_out;  // host outputs (may be empty)
-  std::function<void()> after_round1;             // called once round 1 is synchronised
-};
 
-// out[i] = sum_k coef_k * src_k[i] (zero beyond len_k) + (i == 0 ? c0 : 0), any number of terms:
-// launches of LC_MAX terms, every launch after the first adds the previous partial (out itself,
-// element-wise in place) as its first term
-struct LcTerms {
-  std::vector<const uint32_t*> src;
-  std::vector<uint64_t> len;
-  std::vector<Fr> coef;
-  Fr c0 = Fr::zero();
-  void add(const uint32_t* s, uint64_t l, const Fr& k) {
-    src.push_back(s);
-    len.push_back(l);
-    coef.push_back(k);
-  }
-};
 
 void run_lincomb(hipStream_t st, uint32_t* out, uint64_t n, const LcTerms& t) {
   size_t k = 0;
@@ -705,7 +455,75 @@ void run_lincomb(hipStream_t st, uint32_t* out, uint64_t n, const LcTerms& t) {
   } while (k < t.src.size());
 }
 
+// Round 5 (prover.js:320-413): r(X) + the opening numerator as sum_k coef_k P_k + c0, from the
+// challenges and round-4 evaluations. Z_H(xi), L1(xi) as polynomial_utils.js:1-19. Shared by the
+// single-GPU and the distributed prover.
+R5 round5_terms(bool gs, bool sel, int k, int nbits, const Fr& alpha, const Fr& beta, const Fr& gamma, const Fr& v,
+                const Fr& xi, const std::vector<Fr>& fx, const std::vector<Fr>& tx, const Fr& sFx, const Fr& sTx,
+                const Fr& sxiw) {
+  const uint64_t n = 1ull << nbits;
+  Fr xn = xi;
+  for (int i = 0; i < nbits; i++) xn = xn.sqr();
+  const Fr zh = xn - Fr::one();
+  const Fr l1 = zh * (Fr::from_u64(n) * (xi - Fr::one())).inverse();
+  Fr fxi = Fr::zero(), txi = Fr::zero();
+  for (int i = k - 1; i >= 0; i--) {
+    fxi = fxi * beta + fx[i];
+    if (gs) txi = txi * beta + tx[i];
+  }
+  const Fr one = Fr::one();
+  Fr selBin = Fr::zero();  // alpha^3 selTBin + alpha^2 selFBin
+  if (sel) selBin = ((sTx - sTx.sqr()) * alpha + (sFx - sFx.sqr())) * alpha * alpha;
+  std::vector<Fr> vp(2 * k + 4);
+  vp[0] = one;
+  for (size_t i = 1; i < vp.size(); i++) vp[i] = vp[i - 1] * v;
+  R5 r;
+  Fr c0;
+  if (gs) {
+    const Fr fg = fxi + gamma, tg = txi + gamma;
+    Fr rc = sxiw * fg * tg + (sel ? sTx * fg - sFx * tg : fxi - txi);
+    c0 = selBin + alpha * rc;
+    r.terms.push_back({R5_S, 0, l1 - alpha * fg * tg});
+    r.terms.push_back({R5_Q, 0, zh.neg()});
+    for (int i = 0; i < k; i++) {
+      r.terms.push_back({R5_F, i, vp[1 + i]});
+      c0 = c0 - vp[1 + i] * fx[i];
+    }
+    for (int i = 0; i < k; i++) {
+      r.terms.push_back({R5_T, i, vp[1 + k + i]});
+      c0 = c0 - vp[1 + k + i] * tx[i];
+    }
+    if (sel) {
+      r.terms.push_back({R5_SELF, 0, vp[2 * k + 1]});
+      r.terms.push_back({R5_SELT, 0, vp[2 * k + 2]});
+      c0 = c0 - vp[2 * k + 1] * sFx - vp[2 * k + 2] * sTx;
+    }
+  } else {
+    const Fr fg = fxi + gamma;
+    const Fr dF = sel ? sFx * (fg - one) + one : fg;
+    c0 = selBin + alpha * sxiw * (sel ? sTx * (gamma - one) + one : gamma) - l1;
+    r.terms.push_back({R5_POLT, 0, alpha * sxiw * (sel ? sTx : one)});
+    r.terms.push_back({R5_S, 0, l1 - alpha * dF});
+    r.terms.push_back({R5_Q, 0, zh.neg()});
+    for (int i = 0; i < k; i++) {
+      r.terms.push_back({R5_F, i, vp[1 + i]});
+      c0 = c0 - vp[1 + i] * fx[i];
+    }
+    if (sel) {
+      r.terms.push_back({R5_SELF, 0, vp[k + 1]});
+      r.terms.push_back({R5_SELT, 0, vp[k + 2]});
+      c0 = c0 - vp[k + 1] * sFx - vp[k + 2] * sTx;
+    }
+  }
+  r.c0 = c0;
+  return r;
+}
+
 void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out) {
+  if (c.group) {
+    prove_dist_group(c, in, com_out, ev_out);
+    return;
+  }
   using clk = std::chrono::steady_clock;
   auto t0 = clk::now();
   c.timing.resize(9, 0.0);
@@ -963,63 +781,23 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   }
   tr.add_scalar(sxiw);
   const Fr v = tr.challenge();
-  // Z_H(xi), L1(xi) (polynomial_utils.js)
-  Fr xn = xi;
-  for (int i = 0; i < nbits; i++) xn = xn.sqr();
-  const Fr zh = xn - Fr::one();
-  const Fr l1 = zh * (Fr::from_u64(n) * (xi - Fr::one())).inverse();
-  Fr fxi = Fr::zero(), txi = Fr::zero();
-  for (int i = k - 1; i >= 0; i--) {
-    fxi = fxi * beta + fx[i];
-    if (gs) txi = txi * beta + tx[i];
-  }
-  const Fr one = Fr::one();
-  Fr selBin = Fr::zero();  // alpha^3 selTBin + alpha^2 selFBin
-  if (sel) selBin = ((sTx - sTx.sqr()) * alpha + (sFx - sFx.sqr())) * alpha * alpha;
+  const R5 r5 = round5_terms(gs, sel, k, nbits, alpha, beta, gamma, v, xi, fx, tx, sFx, sTx, sxiw);
   LcTerms lw;
-  Fr c0;
+  for (const R5Term& t : r5.terms) {
+    switch (t.id) {
+      case R5_S: lw.add(Sc, n, t.coef); break;
+      case R5_Q: lw.add(Qc, qlen, t.coef); break;
+      case R5_F: lw.add(Fc[t.idx], n, t.coef); break;
+      case R5_T: lw.add(Tc[t.idx], n, t.coef); break;
+      case R5_SELF: lw.add(sFc, n, t.coef); break;
+      case R5_SELT: lw.add(sTc, n, t.coef); break;
+      case R5_POLT: lw.add(polT, n, t.coef); break;
+    }
+  }
+  lw.c0 = r5.c0;
+  const Fr one = Fr::one();
   uint32_t* Pbuf;
   uint64_t L;
-  std::vector<Fr> vp(2 * k + 4);
-  vp[0] = one;
-  for (size_t i = 1; i < vp.size(); i++) vp[i] = vp[i - 1] * v;
-  if (gs) {
-    const Fr fg = fxi + gamma, tg = txi + gamma;
-    Fr rc = sxiw * fg * tg + (sel ? sTx * fg - sFx * tg : fxi - txi);
-    c0 = selBin + alpha * rc;
-    lw.add(Sc, n, l1 - alpha * fg * tg);
-    lw.add(Qc, qlen, zh.neg());
-    for (int i = 0; i < k; i++) {
-      lw.add(Fc[i], n, vp[1 + i]);
-      c0 = c0 - vp[1 + i] * fx[i];
-    }
-    for (int i = 0; i < k; i++) {
-      lw.add(Tc[i], n, vp[1 + k + i]);
-      c0 = c0 - vp[1 + k + i] * tx[i];
-    }
-    if (sel) {
-      lw.add(sFc, n, vp[2 * k + 1]);
-      lw.add(sTc, n, vp[2 * k + 2]);
-      c0 = c0 - vp[2 * k + 1] * sFx - vp[2 * k + 2] * sTx;
-    }
-  } else {
-    const Fr fg = fxi + gamma;
-    const Fr dF = sel ? sFx * (fg - one) + one : fg;
-    c0 = selBin + alpha * sxiw * (sel ? sTx * (gamma - one) + one : gamma) - l1;
-    lw.add(polT, n, alpha * sxiw * (sel ? sTx : one));
-    lw.add(Sc, n, l1 - alpha * dF);
-    lw.add(Qc, qlen, zh.neg());
-    for (int i = 0; i < k; i++) {
-      lw.add(Fc[i], n, vp[1 + i]);
-      c0 = c0 - vp[1 + i] * fx[i];
-    }
-    if (sel) {
-      lw.add(sFc, n, vp[k + 1]);
-      lw.add(sTc, n, vp[k + 2]);
-      c0 = c0 - vp[k + 1] * sFx - vp[k + 2] * sTx;
-    }
-  }
-  lw.c0 = c0;
   L = qlen > n ? qlen : n;
   Pbuf = c.buf("Pw", 32 * L);
   uint32_t* Wx = c.buf("Wxi", 32 * L);
@@ -1266,13 +1044,10 @@ int kgs_ptau_write_synthetic(kgs_ctx_t* ctx, const char* path, int power, const 
 }
 
 
-namespace {
+}  // extern "C"
+
+namespace kgsi {
 // host copies between pageable caller buffers and the pinned staging area, split over threads
-struct CopyJob {
-  uint8_t* dst;
-  const uint8_t* src;
-  size_t len;
-};
 void par_copy(const std::vector<CopyJob>& jobs) {
   const size_t piece = 1u << 20;
   std::vector<CopyJob> pieces;
@@ -1292,7 +1067,9 @@ void par_copy(const std::vector<CopyJob>& jobs) {
     });
   for (auto& x : th) x.join();
 }
-}  // namespace
+}  // namespace kgsi
+
+extern "C" {
 
 int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* const* evals_f,
               const uint8_t* const* evals_t, const uint8_t* sel_f, const uint8_t* sel_t, uint8_t* const* mont_f,
