@@ -26,8 +26,9 @@ Extra fields in the JSON line:
               PMC FETCH+WRITE from profiles/
   hbm_view  : proof-level bytes (SURVEY.md §8d's count over the reference op list) per second vs 8 TB/s
   extra_configs : BASELINE.json configs[2] (grand-product at n), configs[3] (grand-sum n = 2^24) and
-              configs[4] (selected-vector k = 4, n = 2^22) — single GPU at N = 1, every MSM
-              point-range sharded over all ranks at N > 1 (strong scaling); each checks a proof
+              configs[4] (selected-vector k = 4, n = 2^22) — single GPU at N = 1; at N > 1 ONE proof at
+              a time over all ranks with the distributed prover (every vector sharded; RCCL
+              all-to-all / all-gather; strong scaling); each checks a proof and that ranks agree
   cpu_baseline : the CPU port of the reference op list (oracle/c, OpenMP) on the same workload
 """
 import argparse
@@ -118,11 +119,23 @@ def shared_ptau(ctx, nbits, dist):
     return path, time.time() - t0
 
 
-def large_leg(K, torch, dist, rank, world, local, nb, k, selected, proofs, label):
+def make_group(K, torch, dist, rank, world, local):
+    """Rank group of the distributed prover for N > 1: RCCL (the communicator id made on rank 0 and
+    broadcast through torch.distributed); the gloo rehearsal uses a host all-gather group."""
+    if BACKEND == "gloo":
+        return K.Group.host(world, K.torch_allgather()), "host all-gather group (gloo rehearsal)"
+    uid = K.rccl_unique_id() if rank == 0 else bytes(128)
+    t = torch.tensor(list(uid), dtype=torch.uint8, device=coll_device())
+    dist.broadcast(t, 0)
+    return K.Group.rccl(rank, world, bytes(t.cpu().tolist()), local), "RCCL over xGMI"
+
+
+def large_leg(K, torch, dist, rank, world, local, nb, k, selected, proofs, label, group=None):
     """One large configuration (BASELINE configs[3] / [4]: SURVEY C4 / C5), same inputs on every
-    rank: N = 1 on one GPU; N > 1 with every MSM point-range sharded over all ranks
-    (kgs_ctx_set_shard over torch.distributed = RCCL). The last proof is checked with the native
-    verifier (kgs_verify_ptau: transcript replay + pairing)."""
+    rank: N = 1 on one GPU; N > 1 the distributed prover (kgs_ctx_set_group: every vector sharded —
+    NTTs by all-to-all, builder scan, quotient, Horner, divisions and every MSM on per-rank slices),
+    strong scaling; if no group could be made, MSM point-range sharding only (kgs_ctx_set_shard).
+    The last proof is checked with the native verifier (kgs_verify_ptau: transcript replay + pairing)."""
     n = 1 << nb
     log(f"large leg: {label}")
     ctx = K.Context(local)
@@ -151,8 +164,13 @@ def large_leg(K, torch, dist, rank, world, local, nb, k, selected, proofs, label
         keep += [tsf, tst]
         sfp, stp = tsf.data_ptr(), tst.data_ptr()
         del sf, st
-    if world > 1:
+    mode = "single GPU"
+    if world > 1 and group is not None:
+        ctx.set_group(group[0], rank)
+        mode = f"distributed prover, every vector sharded over {world} ranks ({group[1]}), strong scaling"
+    elif world > 1:
         ctx.set_shard(rank, world, K.torch_allgather(device=None if BACKEND == "gloo" else f"cuda:{local}"))
+        mode = "msm point-range sharded (strong scaling)"
     ctx.prove_device(K.GRANDSUM, nb, d_f, d_t, sfp, stp)  # warm-up
     if dist:
         dist.barrier()
@@ -164,16 +182,17 @@ def large_leg(K, torch, dist, rank, world, local, nb, k, selected, proofs, label
     el = max_over_ranks(time.perf_counter() - t1)
     cn, en = K.proof_names(K.GRANDSUM, k, selected)
     verified = K.grandsum_verifier(ptau, {"commitments": dict(zip(cn, coms)), "evaluations": dict(zip(en, evs))}, nb)
-    out = {"workload": label, "n_gpus": world,
-           "mode": "msm point-range sharded (strong scaling)" if world > 1 else "single GPU",
+    out = {"workload": label, "n_gpus": world, "mode": mode,
            "proofs": proofs, "ms_per_proof": round(1000.0 * el / proofs, 3),
-           "proofs_per_s": round(proofs / el, 4), "srs_setup_s": round(setup_s, 2), "proof_verified": verified}
+           "proofs_per_s": round(proofs / el, 4), "srs_setup_s": round(setup_s, 2), "proof_verified": verified,
+           "round_ms_last_proof_rank0": [round(x, 3) for x in ctx.last_timing()[:5]]}
     if dist:
         h = torch.tensor(list(K.keccak256(b"".join(coms))[:8]), dtype=torch.int64, device=coll_device())
         hs = [torch.empty_like(h) for _ in range(world)]
         dist.all_gather(hs, h)
         out["ranks_agree"] = all(bool(torch.equal(hs[0], x)) for x in hs)
     ctx.set_shard(0, 1)
+    ctx.set_group(None)
     ctx.close()
     del keep
     torch.cuda.empty_cache()
@@ -363,11 +382,21 @@ def main():
         for c in ctxs[1:]:
             c.close()
         ctxs[1:] = []
+        group = None
+        if world > 1:
+            try:
+                group = make_group(K, torch, dist, rank, world, local)
+            except Exception as e:  # fall back to MSM-only sharding rather than losing the legs
+                extra_cfg["group_error"] = str(e)[:200]
         extra_cfg["selected_vector"] = large_leg(K, torch, dist, rank, world, local, args.sv_nbits, 4, True,
-                                                 args.sv_proofs, f"selected-vector grand-sum, n=2^{args.sv_nbits}, k=4, selectors")
+                                                 args.sv_proofs, f"selected-vector grand-sum, n=2^{args.sv_nbits}, k=4, selectors",
+                                                 group)
         if args.c4_nbits > 0:
             extra_cfg["large_grandsum"] = large_leg(K, torch, dist, rank, world, local, args.c4_nbits, 1, False,
-                                                    args.c4_proofs, f"grand-sum, n=2^{args.c4_nbits}, k=1, no selectors")
+                                                    args.c4_proofs, f"grand-sum, n=2^{args.c4_nbits}, k=1, no selectors",
+                                                    group)
+        if group is not None:
+            group[0].close()
 
     if rank != 0:
         if dist:
