@@ -70,12 +70,37 @@ def log(msg):
     """progress on stderr (stdout carries only the JSON line)"""
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
-# v_mad_u64_u32 issue rate of the whole chip: 256 CUs x 4 SIMDs x 64 lanes / 4.97 cycles x 2.4 GHz
-# (measured: profiles/ubench/issue_rates.hip). One bucket add (madd-2008-s in 9 x 29-bit limbs,
-# field29.hpp) issues 1,467 of them: 6 products x 162, 2 squares x 126 (45 symmetric partial
-# products + 81 for the reduction), and Y3 = R*T - Y1*PPP as one lazily reduced double product (243)
-MAD_PEAK = 256 * 4 * 64 / 4.97 * 2.4e9
+# v_mad_u64_u32 issue rate of the whole chip: 256 CUs x 4 SIMDs x 64 lanes / MAD_CYCLES x 2.4 GHz
+# (measured: profiles/ubench/issue_rates.hip; the fastest of the boxes measured). One bucket add
+# (madd-2008-s in 9 x 29-bit limbs, field29.hpp) issues 1,467 of them: 6 products x 162, 2 squares x
+# 126 (45 symmetric partial products + 81 for the reduction), and Y3 = R*T - Y1*PPP as one lazily
+# reduced double product (243)
+MAD_CYCLES = 4.93  # ubench_r02.txt issue_rates (5.25 on the round-1 box: ubench_r01.txt)
+MAD_PEAK = 256 * 4 * 64 / MAD_CYCLES * 2.4e9
 MADS_PER_ADD = 6 * 162 + 2 * 126 + 243
+# mads per 254-bit Montgomery product: 9 x 29-bit CIOS (81 a*b + 81 m*q, the kernel's form) and the
+# representation-neutral floor of 8 x 32-bit limbs (64 + 64 32x32-bit partial products)
+MADS_PER_PRODUCT_29 = 162
+MADS_PER_PRODUCT_32 = 128
+
+
+def roctx_range(name):
+    """roctx range around a bench phase (rocprofv3 --marker-trace), so a kernel trace can be cut to
+    the timed region (profiles/summarize_window.py). No-op without the roctx library."""
+    import contextlib
+    try:
+        lib = ctypes.CDLL("librocprofiler-sdk-roctx.so")
+    except OSError:
+        return contextlib.nullcontext()
+
+    @contextlib.contextmanager
+    def rng():
+        lib.roctxRangePushA(name.encode())
+        try:
+            yield
+        finally:
+            lib.roctxRangePop()
+    return rng()
 
 
 def bench_tau():
@@ -213,6 +238,8 @@ def main():
     ap.add_argument("--no-extra-legs", dest="extra_legs", action="store_false",
                     help="skip the grand-product (configs[2]), grand-sum 2^24 (configs[3]) and selected-vector "
                          "2^22 (configs[4]) legs")
+    ap.add_argument("--no-host-leg", dest="host_leg", action="store_false",
+                    help="skip the host-buffer boundary and JavaScript legs (profiling the timed region)")
     ap.add_argument("--sv-nbits", type=int, default=22)
     ap.add_argument("--c4-nbits", type=int, default=24, help="configs[3] leg (0 = skip)")
     ap.add_argument("--c4-proofs", type=int, default=3)
@@ -310,12 +337,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     log("timed region")
-    ts = time.perf_counter()
-    steps(args.steps)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - ts
+    with roctx_range("kgs_bench_timed_region"):
+        ts = time.perf_counter()
+        steps(args.steps)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        elapsed = time.perf_counter() - ts
     elapsed = max_over_ranks(elapsed)
     total_proofs = args.steps * world
     value = total_proofs / elapsed
@@ -325,7 +353,7 @@ def main():
     # pageable host buffers, including the H2D copy of F/T and the D2H Montgomery write-back
     log(f"timed: {value:.2f} proofs/s; host-buffer and JS legs")
     host_leg = None
-    if rank == 0:
+    if rank == 0 and args.host_leg:
         hf = [synth_evals(n, 1000 * rank + i)[0].tobytes() for i in range(args.npols)]
         ht = [synth_evals(n, 1000 * rank + i)[1].tobytes() for i in range(args.npols)]
         ctx.prove(kind, nbits, hf, ht)  # warm
@@ -432,17 +460,17 @@ def main():
     # ---------------- roofline of the dominant kernel (k_accumulate)
     # The kernel is integer-VALU issue bound. Algorithmic work per launch: entries x 1 mixed XYZZ add
     # (madd-2008-s: 8M + 2S = 10 Fq Montgomery products). Peak: the Fq-product rate at which the
-    # chip's measured v_mad_u64_u32 issue rate (MAD_PEAK: 4.97 SIMD cycles per wave64 instruction at
-    # the 2.4 GHz nominal clock, profiles/ubench/ubench_r01.txt) is spent on nothing but the 162 mads
-    # of a 9 x 29-bit Montgomery product (field29.hpp) — no carries, loads or control. The kernel's own
-    # instruction stream is leaner per add (MADS_PER_ADD: squares and the lazily reduced Y3 save 153
-    # mads) and carries ~40 % non-mad instructions, so frac measures how close the whole add gets to
-    # that mad-only product rate. Timed with HIP events on the MSM's stream around the k_accumulate
-    # launch alone.
+    # chip's measured v_mad_u64_u32 issue rate (MAD_PEAK: MAD_CYCLES SIMD cycles per wave64
+    # instruction at the 2.4 GHz nominal clock, profiles/ubench/) is spent on nothing but the mads of
+    # a product — no carries, loads or control: `peak` for the kernel's 9 x 29-bit product (162
+    # mads), `peak_8x32` for the 128 mads of 8 x 32-bit limbs (the fewest 32x32-bit partial products
+    # a 254-bit Montgomery product can have on this ISA). Timed with HIP events on the MSM's stream
+    # around the k_accumulate launch alone.
     acc_ms = ph[1]
     mults = 10 * entries.value
     achieved = mults / (acc_ms / 1e3) / 1e9
-    peak = MAD_PEAK / 162 / 1e9
+    peak = MAD_PEAK / MADS_PER_PRODUCT_29 / 1e9
+    peak32 = MAD_PEAK / MADS_PER_PRODUCT_32 / 1e9
     traffic = None
     pmc_path = os.path.join(HERE, "profiles", "pmc_accumulate.json")
     if os.path.exists(pmc_path):
@@ -452,7 +480,10 @@ def main():
         except Exception:
             traffic = None
     roofline = {"bound": "valu", "kernel": "k_accumulate", "achieved": round(achieved, 2), "peak": round(peak, 2),
-                "unit": "G Fq-products/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                "unit": "G Fq-products/s", "frac": round(achieved / peak, 4),
+                "peak_8x32": round(peak32, 2), "frac_8x32": round(achieved / peak32, 4), "traffic": traffic,
+                "peak_note": f"v_mad_u64_u32 issue rate ({MAD_CYCLES} SIMD cycles per wave64 instruction, 256 CUs x 4 "
+                             f"SIMDs, 2.4 GHz) / mads per product: 162 (9 x 29-bit, peak) or 128 (8 x 32-bit, peak_8x32)",
                 "bound_note": "integer-VALU issue bound (254-bit Montgomery products on v_mad_u64_u32): neither the "
                               "HBM roof (the kernel moves ~1 TB/s of 8) nor MFMA (no dense contraction) applies",
                 "mad_issue_frac": round(entries.value * MADS_PER_ADD / (acc_ms / 1e3) / MAD_PEAK, 4),

@@ -104,9 +104,12 @@ void launch_div_fix(hipStream_t st, uint32_t* q, const uint32_t* pz, const uint3
 // msm.hip
 void msm_build_table(hipStream_t st, uint32_t* table, uint64_t npts, int c, int W, uint32_t* tmp_xyzz,
                      uint32_t* scratch);
-// scalars[i] multiplies SRS point pbase + pstride * i (pbase + pstride * (N - 1) < tb.npts)
+// scalars[i] multiplies SRS point pbase + pstride * i (pbase + pstride * (N - 1) < tb.npts).
+// exclusive_acc: the bucket accumulation takes a SIMD's whole register file at its two waves (for a
+// context whose two MSM lanes would otherwise co-run their accumulations and delay each other's
+// tails); default: a 168-VGPR build that leaves room for other proofs' kernels (msm.hip).
 void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* scalars, uint64_t N, uint32_t* T_out,
-             hipEvent_t* ev = nullptr, uint64_t pbase = 0, uint64_t pstride = 1);
+             hipEvent_t* ev = nullptr, uint64_t pbase = 0, uint64_t pstride = 1, bool exclusive_acc = false);
 void launch_fixed_base(hipStream_t st, uint32_t* out_xyzz, const uint32_t* sc, uint64_t count, const uint32_t* tbl);
 void launch_batch_affine(hipStream_t st, uint32_t* out_aff, const uint32_t* in_xyzz, uint32_t* scratch, uint64_t npts);
 

@@ -421,12 +421,21 @@ __device__ __forceinline__ const uint32_t* run_rec(const uint32_t* raw, uint64_t
 #ifndef KGS_ACC_WAVES
 #define KGS_ACC_WAVES 2
 #endif
+// Register budget of the add loop (template VW): the default build is compiled for 3 waves/SIMD
+// (<= 168 VGPRs) although launched at KGS_ACC_WAVES, so two resident accumulate waves leave 176 of a
+// SIMD's 512 VGPRs and the other in-flight proofs' kernels of up to 176 VGPRs (the MSM tail's
+// combine levels at 162, NTT passes, divisions) co-reside instead of waiting for a whole accumulate
+// launch to drain: +1.9 % proofs/s (same-box A/B). A context running two MSM lanes uses the VW = 2
+// build (169 VGPRs -> 176 allocated, the whole register file at two waves): its second lane's
+// accumulation then waits for the first instead of co-running with it, so the first lane's tail runs
+// beside the second lane's accumulation (single-proof latency 16.3 -> 14.8 ms).
 // diagnostic builds only (wrong results): KGS_DIAG_GATHER_MASK confines the point gathers to a small,
 // cache-resident part of the table, to measure what the random HBM gathers cost the add loop
 #ifndef KGS_DIAG_GATHER_MASK
 #define KGS_DIAG_GATHER_MASK 0x7fffffffu
 #endif
-__global__ void __launch_bounds__(256, KGS_ACC_WAVES) k_accumulate(uint32_t* __restrict__ segowner,
+template <int VW>
+__global__ void __launch_bounds__(256, VW) k_accumulate(uint32_t* __restrict__ segowner,
                                                     uint32_t* __restrict__ chunklist, uint32_t* __restrict__ chunkcnt,
                                                     const uint32_t* __restrict__ sorted,
                                                     const uint32_t* __restrict__ offsets, uint32_t nbins,
@@ -613,7 +622,7 @@ __global__ void __launch_bounds__(128) k_bitsum_rc(uint32_t* __restrict__ T, con
 
 // ------------------------------------------------------------------ driver (device part)
 void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* scalars, uint64_t N,
-             uint32_t* T_out, hipEvent_t* ev, uint64_t pbase, uint64_t pstride) {
+             uint32_t* T_out, hipEvent_t* ev, uint64_t pbase, uint64_t pstride, bool exclusive_acc) {
   // ev (optional, 5 events): [0] start, [1] after digits+sort, [2] after k_accumulate,
   // [3] after combine, [4] after bit-sum reduction
   if (ev) hipEventRecord(ev[0], st);
@@ -667,8 +676,12 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   uint32_t* cnt = w.chunkcnt;
   const uint64_t lcap = nseg / CB_T + B + 16;
   hipMemsetAsync(cnt, 0, 4 * CB_LEVELS, st);
-  hipLaunchKernelGGL(k_accumulate, dim3(nb(nseg)), dim3(256), 0, st, w.segowner, w.chunklist, cnt, w.sorted,
-                     w.offsets, B + 1, tb.table, (uint32_t)L, w.raw29);
+  if (exclusive_acc)
+    hipLaunchKernelGGL(k_accumulate<2>, dim3(nb(nseg)), dim3(256), 0, st, w.segowner, w.chunklist, cnt, w.sorted,
+                       w.offsets, B + 1, tb.table, (uint32_t)L, w.raw29);
+  else
+    hipLaunchKernelGGL(k_accumulate<3>, dim3(nb(nseg)), dim3(256), 0, st, w.segowner, w.chunklist, cnt, w.sorted,
+                       w.offsets, B + 1, tb.table, (uint32_t)L, w.raw29);
   if (ev) hipEventRecord(ev[2], st);  // the accumulate phase is the k_accumulate launch alone
   uint64_t stride = 1, cap = lcap;
   for (int j = 0; j < CB_LEVELS; j++, stride *= CB_T) {

@@ -209,17 +209,23 @@ __global__ void __launch_bounds__(256) k_builder_finish(uint32_t* __restrict__ o
   __shared__ uint32_t lds[256 * 8];
   const fr g = fr::load(gp);
   const uint64_t base = (uint64_t)blockIdx.x * BT_TILE + threadIdx.x * BT_PER;
-  fr num[BT_PER], den[BT_PER];
+  // np[r] = num_r * (product of this thread's nonzero den_k, k < r), so that the backward pass needs
+  // one product per element for s_r = num_r / den_r (np[r] * inv) and one to step inv: 4 products
+  // per element instead of 5, and no separate num / prefix arrays (fits 176 VGPRs: co-resides with
+  // the MSM bucket accumulation of other proofs in flight)
+  fr np[BT_PER], den[BT_PER];
   fr p = fr::one();
 #pragma unroll
   for (int r = 0; r < BT_PER; r++) {
     uint64_t i = base + r;
+    fr num;
     if (i < n) {
-      numden<PROD, SEL>(i, f, t, sf, st_, g, num[r], den[r]);
+      numden<PROD, SEL>(i, f, t, sf, st_, g, num, den[r]);
     } else {
-      num[r] = PROD ? fr::one() : fr::zero();
+      num = PROD ? fr::one() : fr::zero();
       den[r] = fr::one();
     }
+    np[r] = num * p;
     if (!den[r].is_zero()) p = p * den[r];
   }
   // exclusive prefix/suffix of thread products inside the tile
@@ -234,25 +240,15 @@ __global__ void __launch_bounds__(256) k_builder_finish(uint32_t* __restrict__ o
   fr sex = threadIdx.x < 255 ? fr::load(lds + 8 * (threadIdx.x + 1)) : fr::one();
   __syncthreads();
   fr inv = fr::load(tinv + 8 * (uint64_t)blockIdx.x) * pex * sex;  // 1/p
-  // backward: den_r^-1 = inv * prefix_{r-1}; recompute prefixes on the fly (store them in num? no:
-  // keep a small register array of prefixes)
-  fr pre[BT_PER];
-  fr run = fr::one();
-#pragma unroll
-  for (int r = 0; r < BT_PER; r++) {
-    pre[r] = run;
-    if (!den[r].is_zero()) run = run * den[r];
-  }
-  fr s[BT_PER];
+  // backward: inv = 1 / (prefix_r * den_r) before step r, so num_r / den_r = np[r] * inv
+  fr* s = np;  // s_r overwrites np[r]
 #pragma unroll
   for (int r = BT_PER - 1; r >= 0; r--) {
     if (den[r].is_zero()) {
       s[r] = fr::zero();  // batchInverse(0) = 0 -> term 0
-      if (PROD) s[r] = fr::zero();
     } else {
-      fr dinv = inv * pre[r];
+      s[r] = np[r] * inv;
       inv = inv * den[r];
-      s[r] = num[r] * dinv;
     }
   }
   // local inclusive scan inside thread, then across the tile

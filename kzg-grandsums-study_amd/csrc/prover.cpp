@@ -315,7 +315,7 @@ Commit commit_launch_slice(kgs_ctx& c, const uint32_t* scalars, uint64_t count, 
   }
   if (c.msm_lanes < 2) lane = 0;
   hipStream_t st = lane ? c.st2 : c.st;  // lane 1 was forked (fork_lanes) after the round's inputs
-  msm_run(st, c.tb, lane ? c.mw2 : c.mw, scalars, count, dT, nullptr, pbase, pstride);
+  msm_run(st, c.tb, lane ? c.mw2 : c.mw, scalars, count, dT, nullptr, pbase, pstride, c.msm_lanes >= 2);
   check_launch();
   HC(hipMemcpyAsync(cm.h_T, dT, (size_t)cc * 128, hipMemcpyDeviceToHost, st));
   return cm;
