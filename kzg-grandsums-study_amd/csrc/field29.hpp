@@ -236,11 +236,9 @@ struct fq29 {
   }
 
   // necessary condition for "== 0 mod q" of a normalised value < 8q: its low limb is (j*q) mod 2^29
+  // for some j < 8, i.e. l0 * q0^-1 mod 2^29 < 8 (q0 is odd; q0^-1 = -INV): 3 instructions
   __device__ __forceinline__ bool maybe_zero8() const {
-    bool z = false;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; j++) z |= l[0] == ((j * f29::Q.v[0]) & f29::MASK);
-    return z;
+    return ((l[0] * (0u - f29::INV)) & f29::MASK) < 8u;
   }
   // x*2^261 -> canonical fq (x*2^256), for a normalised value with value*2^253.6 < 2^261*q
   __device__ __forceinline__ fq to_fq() const {
