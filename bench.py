@@ -416,13 +416,20 @@ def main():
                 group = make_group(K, torch, dist, rank, world, local)
             except Exception as e:  # fall back to MSM-only sharding rather than losing the legs
                 extra_cfg["group_error"] = str(e)[:200]
-        extra_cfg["selected_vector"] = large_leg(K, torch, dist, rank, world, local, args.sv_nbits, 4, True,
-                                                 args.sv_proofs, f"selected-vector grand-sum, n=2^{args.sv_nbits}, k=4, selectors",
-                                                 group)
+        def leg(*a):
+            # a failing leg must not lose the headline line: a library failure on one rank aborts the
+            # rank group, so every rank raises here and they stay in step
+            try:
+                return large_leg(K, torch, dist, rank, world, local, *a, group)
+            except Exception as e:
+                log(f"leg failed: {e}")
+                torch.cuda.synchronize()
+                return {"workload": a[4], "error": str(e)[:300]}
+        extra_cfg["selected_vector"] = leg(args.sv_nbits, 4, True, args.sv_proofs,
+                                           f"selected-vector grand-sum, n=2^{args.sv_nbits}, k=4, selectors")
         if args.c4_nbits > 0:
-            extra_cfg["large_grandsum"] = large_leg(K, torch, dist, rank, world, local, args.c4_nbits, 1, False,
-                                                    args.c4_proofs, f"grand-sum, n=2^{args.c4_nbits}, k=1, no selectors",
-                                                    group)
+            extra_cfg["large_grandsum"] = leg(args.c4_nbits, 1, False, args.c4_proofs,
+                                              f"grand-sum, n=2^{args.c4_nbits}, k=1, no selectors")
         if group is not None:
             group[0].close()
 

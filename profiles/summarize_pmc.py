@@ -39,7 +39,7 @@ def main():
     with open(os.path.join(HERE, f"pmc_{tag}.json"), "w") as fh:
         json.dump({"round": tag, "kernels": kernels}, fh, indent=1)
     # run on profiles/msm_loop.py (every MSM is a 2^20-point one): the k_accumulate dispatches
-    acc = [k for k in kernels if k["kernel"].endswith("k_accumulate")]
+    acc = [k for k in kernels if k["kernel"].split("<")[0].endswith("k_accumulate")]
     if acc:
         a = acc[0]
         with open(os.path.join(HERE, "pmc_accumulate.json"), "w") as fh:
