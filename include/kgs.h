@@ -169,6 +169,11 @@ int kgs_verify(int kind, int nbits, int npols, int selected, const uint8_t* comm
                const uint8_t tau_g2[128]);
 int kgs_verify_ptau(int kind, const char* ptau_path, int nbits, int npols, int selected, const uint8_t* commitments,
                     const uint8_t* evaluations);
+/* curve.pairingEq (src/grandsum/mset_eq_kzg_verifier.js:182, src/grandproduct/mset_eq_kzg_verifier.js:177;
+ * [ffjs] bn128 optimal-ate pairing): 1 if prod_k e(P_k, Q_k) == 1, 0 if not. P_k: affine LEM G1
+ * (64 B, Montgomery; (0, 0) = infinity), Q_k: affine LEM G2 (128 B: x.c0, x.c1, y.c0, y.c1). Points
+ * off their curve: KGS_E_ARG. Host only. */
+int kgs_pairing_eq(int npairs, const uint8_t* g1_lem, const uint8_t* g2_lem);
 
 /* Per-proof timing of the last kgs_prove* call (milliseconds, host wall clock): [0..4] prover rounds
  * 1-5, [5] unused, and for kgs_prove (host buffers) [6] input copy into pinned staging, [7] the

@@ -252,18 +252,28 @@ inline Fq12 final_exp(const Fq12& f) {
   return f2.pow(E_HARD, 12);             // ^((q^4 - q^2 + 1) / r)
 }
 
-// curve.pairingEq(a1, b1, a2, b2): e(a1, b1) * e(a2, b2) == 1; G1 points as host XYZZ
-inline bool pairing_eq2(const G1& a1, const G2A& b1, const G1& a2, const G2A& b2) {
+// curve.pairingEq(a1, b1, ..., an, bn): prod_k e(a_k, b_k) == 1 (one final exponentiation); G1
+// points as host XYZZ, G2 affine
+inline bool pairing_eq(const G1* const* as, const G2A* const* bs, int n) {
   Fq12 f = Fq12::one();
-  const G1* as[2] = {&a1, &a2};
-  const G2A* bs[2] = {&b1, &b2};
-  for (int k = 0; k < 2; k++) {
+  for (int k = 0; k < n; k++) {
     if (as[k]->is_inf() || bs[k]->inf) continue;  // e(O, Q) = e(P, O) = 1
     uint8_t lem[64];
     as[k]->to_affine_lem(lem);
     f = f * miller_loop(Fq::from_bytes(lem), Fq::from_bytes(lem + 32), *bs[k]);
   }
   return final_exp(f).is_one();
+}
+inline bool pairing_eq2(const G1& a1, const G2A& b1, const G1& a2, const G2A& b2) {
+  const G1* as[2] = {&a1, &a2};
+  const G2A* bs[2] = {&b1, &b2};
+  return pairing_eq(as, bs, 2);
+}
+// y^2 = x^3 + 3 for an affine LEM G1 point (the zero point (0, 0) is valid)
+inline bool g1_lem_on_curve(const uint8_t lem[64]) {
+  Fq x = Fq::from_bytes(lem), y = Fq::from_bytes(lem + 32);
+  if (x.is_zero() && y.is_zero()) return true;
+  return y.sqr() == x.sqr() * x + Fq::from_u64(3);
 }
 
 }  // namespace host

@@ -229,6 +229,28 @@ int kgs_verify(int kind, int nbits, int npols, int selected, const uint8_t* comm
   }
 }
 
+int kgs_pairing_eq(int npairs, const uint8_t* g1_lem, const uint8_t* g2_lem) {
+  if (npairs < 0 || npairs > 4096 || (npairs && (!g1_lem || !g2_lem))) return KGS_E_ARG;
+  try {
+    std::vector<host::G1> a(npairs);
+    std::vector<host::G2A> b(npairs);
+    std::vector<const host::G1*> pa(npairs);
+    std::vector<const host::G2A*> pb(npairs);
+    for (int k = 0; k < npairs; k++) {
+      const uint8_t* p1 = g1_lem + 64 * (size_t)k;
+      if (!host::g1_lem_on_curve(p1)) return KGS_E_ARG;
+      a[k] = host::G1::from_affine_lem(p1);
+      b[k] = host::g2_from_lem(g2_lem + 128 * (size_t)k);
+      if (!host::g2_on_curve(b[k])) return KGS_E_ARG;
+      pa[k] = &a[k];
+      pb[k] = &b[k];
+    }
+    return host::pairing_eq(pa.data(), pb.data(), npairs) ? 1 : 0;
+  } catch (const std::exception&) {
+    return KGS_E_ARG;
+  }
+}
+
 int kgs_verify_ptau(int kind, const char* ptau_path, int nbits, int npols, int selected, const uint8_t* commitments,
                     const uint8_t* evaluations) {
   uint8_t t2[128];

@@ -440,6 +440,53 @@ static napi_value VerifyPtau(napi_env env, napi_callback_info info) {
   return out;
 }
 
+// pairingEq(g1s, g2s): g1s = n x 64 B affine LEM G1, g2s = n x 128 B affine LEM G2 -> bool
+// (curve.pairingEq, src/grandsum/mset_eq_kzg_verifier.js:182)
+static napi_value PairingEq(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  std::vector<uint8_t> a = bytes_of(env, argv[0]), b = bytes_of(env, argv[1]);
+  if (a.size() % 64 || b.size() % 128 || a.size() / 64 != b.size() / 128) {
+    napi_throw_error(env, nullptr, "pairingEq: expected n x 64 B G1 and n x 128 B G2 affine points");
+    return nullptr;
+  }
+  const int rc = kgs_pairing_eq((int)(a.size() / 64), a.data(), b.data());
+  if (rc < 0) {
+    napi_throw_error(env, nullptr, "pairingEq: point not on the curve");
+    return nullptr;
+  }
+  napi_value out;
+  napi_get_boolean(env, rc == 1, &out);
+  return out;
+}
+
+// msmPoints(ctx, bases, scalarsStd) -> 64 B affine LEM sum_i s_i P_i on the GPU of ctx (the
+// curve shim's G1.multiExpAffine, polynomial.js:1112, whose scalars are standard-form LE after
+// Fr.batchFromMontgomery): the bases become ctx's resident point set
+static napi_value MsmPoints(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  kgs_ctx_t* ctx = get_ctx(env, argv[0]);
+  std::vector<uint8_t> bases = bytes_of(env, argv[1]), sc = bytes_of(env, argv[2]);
+  const uint64_t n = sc.size() / 32;
+  if (sc.size() % 32 || bases.size() != 64 * n || n < 2) {
+    napi_throw_error(env, nullptr, "msmPoints: expected n >= 2 affine LEM bases and n 32 B scalars");
+    return nullptr;
+  }
+  int lg = 0;
+  while ((1ull << (lg + 1)) < n) lg++;
+  uint8_t out[64];
+  std::vector<uint8_t> mont(sc.size());
+  if (kgs_srs_load_points(ctx, bases.data(), n, lg, lg) != KGS_OK ||
+      kgs_fr_to_mont(ctx, sc.data(), mont.data(), n) != KGS_OK || kgs_msm(ctx, mont.data(), n, out) != KGS_OK) {
+    napi_throw_error(env, nullptr, kgs_last_error());
+    return nullptr;
+  }
+  return make_u8(env, out, 64);
+}
+
 static napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor desc[] = {
       {"ctxCreate", nullptr, CtxCreate, nullptr, nullptr, nullptr, napi_default, nullptr},
@@ -450,6 +497,8 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"verifyPtau", nullptr, VerifyPtau, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"ptauPower", nullptr, PtauPower, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"pairingEq", nullptr, PairingEq, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"msmPoints", nullptr, MsmPoints, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(desc) / sizeof(desc[0]), desc);
   return exports;

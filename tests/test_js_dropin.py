@@ -107,3 +107,85 @@ def test_reference_style_cases():
     out = subprocess.check_output([NODE, os.path.join(JS, "test", "reference_style.test.js"), common.oracle_ptau(9)],
                                   timeout=600)
     assert b"reference-style cases passed: 8" in out
+
+
+def _node_json(script):
+    out = subprocess.check_output([NODE, "-e", script], cwd=JS)
+    return json.loads(out.decode())
+
+
+def test_curve_shim_g1_g2_pairing():
+    """The shim's G1 arithmetic and encodings against the oracle's BN254 (the ffjs conventions:
+    Montgomery LE Jacobian / affine buffers, toRprUncompressed with the 0x40 zero flag), and
+    curve.pairingEq through the native pairing (kgs_pairing_eq, host only)."""
+    from oracle import bn254 as bn
+    a, b = 0x1234567890ABCDEF1234567890ABCDEF, 987654321987654321
+    qb = bn.g2_to_lem(bn.g2_mul(bn.G2_GEN, b)).hex()
+    script = f"""
+const {{ getCurveFromName }} = require('./src/curve.js');
+getCurveFromName('bn128').then(async c => {{
+  const {{ G1, G2, Fr }} = c;
+  const hex = x => Buffer.from(x).toString('hex');
+  const Pa = G1.timesFr(G1.one, Fr.e({a}n)), Pb = G1.timesFr(G1.one, Fr.e({b}n));
+  const Pab = G1.timesFr(G1.one, Fr.e({a * b}n));
+  const rpr = new Uint8Array(64), rz = new Uint8Array(64);
+  G1.toRprUncompressed(rpr, 0, Pa);
+  G1.toRprUncompressed(rz, 0, G1.zero);
+  const Qb = new Uint8Array(Buffer.from('{qb}', 'hex'));
+  const sumAff = G1.toAffine(G1.add(G1.toAffine(Pa), Pb));
+  out = {{
+    a: hex(G1.toAffine(Pa)), sum: hex(sumAff), dbl: hex(G1.toAffine(G1.double(Pa))),
+    sub0: G1.isZero(G1.sub(Pa, Pa)), negsum: G1.isZero(G1.add(Pa, G1.neg(Pa))),
+    eqj: G1.eq(Pa, G1.toAffine(Pa)), valid: G1.isValid(Pa), one: hex(G1.toAffine(G1.one)),
+    rpr: hex(rpr), rz: hex(rz), zeroAff: hex(G1.toAffine(G1.zero)),
+    back: hex(G1.toAffine(G1.fromRprUncompressed(rpr, 0))),
+    pe_ok: await c.pairingEq(G1.neg(Pab), G2.one, Pa, Qb),
+    pe_bad: await c.pairingEq(G1.neg(Pab), G2.one, Pb, Qb),
+    pe_zero: await c.pairingEq(G1.zero, G2.one),
+    small: hex(G1.toAffine(await G1.multiExpAffine(new Uint8Array([...G1.toAffine(Pa), ...G1.toAffine(Pb)]),
+      new Uint8Array([...Fr.fromMontgomery(Fr.e(3n)), ...Fr.fromMontgomery(Fr.e(5n))])))),
+  }};
+  process.stdout.write(JSON.stringify(out));
+}});
+"""
+    o = _node_json(script)
+    G = bn.G1_GEN
+    Pa, Pb = bn.g1_mul(G, a), bn.g1_mul(G, b)
+    assert bytes.fromhex(o["a"]) == bn.g1_to_lem(Pa)
+    assert bytes.fromhex(o["sum"]) == bn.g1_to_lem(bn.g1_add(Pa, Pb))
+    assert bytes.fromhex(o["dbl"]) == bn.g1_to_lem(bn.g1_add(Pa, Pa))
+    assert o["sub0"] and o["negsum"] and o["eqj"] and o["valid"]
+    assert bytes.fromhex(o["one"]) == bn.g1_to_lem(G)
+    assert bytes.fromhex(o["rpr"]) == bn.g1_to_rpr_uncompressed(Pa)
+    assert bytes.fromhex(o["rz"]) == bn.g1_to_rpr_uncompressed(None)
+    assert bytes.fromhex(o["zeroAff"]) == bytes(64)
+    assert bytes.fromhex(o["back"]) == bn.g1_to_lem(Pa)
+    assert o["pe_ok"] is True and o["pe_bad"] is False and o["pe_zero"] is True
+    assert bytes.fromhex(o["small"]) == bn.g1_to_lem(bn.g1_add(bn.g1_mul(Pa, 3), bn.g1_mul(Pb, 5)))
+
+
+@pytest.mark.gpu
+def test_curve_shim_multiexp_on_gpu(tmp_path):
+    """G1.multiExpAffine (polynomial.js:1112) of the shim over arbitrary bases runs on the GPU
+    (kgs_msm over the given points) and matches the oracle's sum."""
+    import random
+    from oracle import bn254 as bn
+    rnd = random.Random(7)
+    n = 1000
+    ks = [rnd.randrange(1, bn.R) for _ in range(n)]
+    ss = [rnd.randrange(bn.R) for _ in range(n)]
+    bases = b"".join(bn.g1_to_lem(bn.g1_mul(bn.G1_GEN, k)) for k in ks)
+    scal = b"".join(s.to_bytes(32, "little") for s in ss)
+    want = bn.g1_to_lem(bn.g1_mul(bn.G1_GEN, sum(k * s for k, s in zip(ks, ss)) % bn.R))
+    (tmp_path / "bases.bin").write_bytes(bases)
+    (tmp_path / "scalars.bin").write_bytes(scal)
+    script = f"""
+const fs = require('fs');
+const {{ getCurveFromName }} = require('./src/curve.js');
+getCurveFromName('bn128').then(async c => {{
+  const r = await c.G1.multiExpAffine(new Uint8Array(fs.readFileSync('{tmp_path / "bases.bin"}')),
+                                      new Uint8Array(fs.readFileSync('{tmp_path / "scalars.bin"}')));
+  process.stdout.write(JSON.stringify({{ r: Buffer.from(c.G1.toAffine(r)).toString('hex') }}));
+}});
+"""
+    assert bytes.fromhex(_node_json(script)["r"]) == want
