@@ -426,9 +426,11 @@ __device__ __forceinline__ const uint32_t* run_rec(const uint32_t* raw, uint64_t
 // SIMD's 512 VGPRs and the other in-flight proofs' kernels of up to 176 VGPRs (the MSM tail's
 // combine levels at 162, NTT passes, divisions) co-reside instead of waiting for a whole accumulate
 // launch to drain: +1.9 % proofs/s (same-box A/B). A context running two MSM lanes uses the VW = 2
-// build (169 VGPRs -> 176 allocated, the whole register file at two waves): its second lane's
-// accumulation then waits for the first instead of co-running with it, so the first lane's tail runs
-// beside the second lane's accumulation (single-proof latency 16.3 -> 14.8 ms).
+// build, which reserves 176 VGPRs (v175 is clobbered, whatever the compiler needs): two waves then
+// take a SIMD's whole register file, its second lane's accumulation waits for the first instead of
+// co-running with it (its blocks start as the first lane's finish), and the first lane's tail runs
+// beside the second lane's accumulation (single-proof latency 16.0 -> 14.8 ms; ordering the two
+// accumulations with events instead measured 15.2-16.5 ms: no block-level hand-over).
 // diagnostic builds only (wrong results): KGS_DIAG_GATHER_MASK confines the point gathers to a small,
 // cache-resident part of the table, to measure what the random HBM gathers cost the add loop
 #ifndef KGS_DIAG_GATHER_MASK
@@ -441,6 +443,7 @@ __global__ void __launch_bounds__(256, VW) k_accumulate(uint32_t* __restrict__ s
                                                     const uint32_t* __restrict__ offsets, uint32_t nbins,
                                                     const uint32_t* __restrict__ table, uint32_t L,
                                                     uint32_t* __restrict__ raw) {
+  if (VW == 2) asm volatile("; reserve v175 (176 VGPRs: two waves per SIMD)" ::: "v175");
   const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t E = offsets[nbins];
   const uint64_t start = s * L;
