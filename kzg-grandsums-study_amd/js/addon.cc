@@ -272,6 +272,7 @@ struct Job {
   std::vector<uint8_t> com, ev;
   std::vector<napi_ref> refs;
   bool selected = false;
+  bool want_mont = true;  // false: no Montgomery write-back (the other ranks of a distributed proof)
 };
 
 static void job_execute(napi_env, void* data) {
@@ -290,9 +291,11 @@ static void job_execute(napi_env, void* data) {
       ok &= j->f[i].len == E && j->t[i].len == E;
       fp.push_back(j->f[i].p);
       tp.push_back(j->t[i].p);
-      j->mf.push_back(out_alloc(E));
-      j->mt.push_back(out_alloc(E));
-      ok &= j->mf.back() && j->mt.back();
+      if (j->want_mont) {
+        j->mf.push_back(out_alloc(E));
+        j->mt.push_back(out_alloc(E));
+        ok &= j->mf.back() && j->mt.back();
+      }
     }
     if (j->selected) ok &= j->sf.len == E && j->st.len == E;
     if (!ok) {
@@ -301,7 +304,8 @@ static void job_execute(napi_env, void* data) {
       return;
     }
     j->rc = kgs_prove(j->ctx, j->kind, j->nbits, j->npols, fp.data(), tp.data(), j->selected ? j->sf.p : nullptr,
-                      j->selected ? j->st.p : nullptr, j->mf.data(), j->mt.data(), j->com.data(), j->ev.data());
+                      j->selected ? j->st.p : nullptr, j->want_mont ? j->mf.data() : nullptr,
+                      j->want_mont ? j->mt.data() : nullptr, j->com.data(), j->ev.data());
   }
   if (j->rc != KGS_OK) j->err = kgs_last_error();
 }
@@ -375,10 +379,11 @@ static napi_value SrsLoad(napi_env env, napi_callback_info info) {
   return queue(env, j, "kgs_srs_load");
 }
 
-// prove(ctx, kind, nbits, [F...], [T...], selF|null, selT|null) -> Promise<{commitments, evaluations, montF, montT}>
+// prove(ctx, kind, nbits, [F...], [T...], selF|null, selT|null[, wantMont = true])
+//   -> Promise<{commitments, evaluations, montF, montT}> (montF/montT empty without wantMont)
 static napi_value Prove(napi_env env, napi_callback_info info) {
-  size_t argc = 7;
-  napi_value argv[7];
+  size_t argc = 8;
+  napi_value argv[8];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
   Job* j = new Job();
   j->op = 1;
@@ -402,6 +407,10 @@ static napi_value Prove(napi_env env, napi_callback_info info) {
     j->selected = true;
     j->sf = view_of(env, argv[5], j->refs);
     j->st = view_of(env, argv[6], j->refs);
+  }
+  if (argc > 7) {
+    napi_typeof(env, argv[7], &ty);
+    if (ty == napi_boolean) napi_get_value_bool(env, argv[7], &j->want_mont);
   }
   return queue(env, j, "kgs_prove");
 }
@@ -438,6 +447,43 @@ static napi_value VerifyPtau(napi_env env, napi_callback_info info) {
   napi_value out;
   napi_get_boolean(env, rc == 1, &out);
   return out;
+}
+
+// groupCreateLocal(world) -> rank group of `world` contexts in this process (kgs_group_create_local):
+// the distributed prover with every vector sharded, driven from one Node process (one libuv
+// thread per rank). ctxSetGroup(ctx, group|null, rank) attaches / detaches a context.
+static void group_finalize(napi_env, void* data, void*) { kgs_group_destroy((kgs_group_t*)data); }
+static napi_value GroupCreateLocal(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  int32_t world = 1;
+  if (argc > 0) napi_get_value_int32(env, argv[0], &world);
+  kgs_group_t* g = nullptr;
+  if (kgs_group_create_local(world, &g) != KGS_OK) {
+    napi_throw_error(env, nullptr, kgs_last_error());
+    return nullptr;
+  }
+  napi_value ext;
+  NAPI_CALL(env, napi_create_external(env, g, group_finalize, nullptr, &ext));
+  return ext;
+}
+static napi_value CtxSetGroup(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  kgs_ctx_t* ctx = get_ctx(env, argv[0]);
+  napi_valuetype ty;
+  napi_typeof(env, argv[1], &ty);
+  void* g = nullptr;
+  if (ty == napi_external) napi_get_value_external(env, argv[1], &g);
+  int32_t rank = 0;
+  if (argc > 2) napi_get_value_int32(env, argv[2], &rank);
+  if (kgs_ctx_set_group(ctx, (kgs_group_t*)g, rank) != KGS_OK) {
+    napi_throw_error(env, nullptr, kgs_last_error());
+    return nullptr;
+  }
+  return nullptr;
 }
 
 // pairingEq(g1s, g2s): g1s = n x 64 B affine LEM G1, g2s = n x 128 B affine LEM G2 -> bool
@@ -498,6 +544,8 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"ptauPower", nullptr, PtauPower, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"pairingEq", nullptr, PairingEq, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"groupCreateLocal", nullptr, GroupCreateLocal, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"ctxSetGroup", nullptr, CtxSetGroup, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"msmPoints", nullptr, MsmPoints, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(desc) / sizeof(desc[0]), desc);

@@ -9,7 +9,8 @@
 // contexts of a device, so a pool of several contexts costs one set of tables per GPU.
 //
 // Knobs: KGS_JS_CONTEXTS = contexts per device (default 4: the proofs in flight that keep one
-// MI355X busy), KGS_DEVICES = comma-separated device list (default: every visible device).
+// MI355X busy), KGS_DEVICES = comma-separated device list (default: every visible device),
+// KGS_JS_SHARD_RANKS / KGS_JS_SHARD_MIN_NBITS = one large proof over several GPUs (below).
 const path = require("path");
 
 // N-API async work runs on the libuv thread pool (4 threads by default): one thread per context of
@@ -83,10 +84,59 @@ function ptauPower(pTauFilename) {
 // and prove on the same held context: nothing can swap the SRS between the two
 async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT) {
     const key = path.resolve(pTauFilename);
+    if (shardRanks() >= 2 && nBits >= shardMinBits()) return proveSharded(kind, key, nBits, evalsF, evalsT, selF, selT);
     return withContext(async slot => {
         await load().srsLoadPtau(slot.ctx, key, nBits);
         return load().prove(slot.ctx, kind, nBits, evalsF, evalsT, selF, selT);
     });
+}
+
+// Large proofs over several GPUs from this one Node process: with KGS_JS_SHARD_RANKS = W >= 2, a
+// proof of at least 2^KGS_JS_SHARD_MIN_NBITS elements (default 22) runs on W contexts (rank r on
+// device r mod #devices) joined by an in-process rank group (kgs_group_create_local +
+// kgs_ctx_set_group): every vector of the proof sharded, NTTs as rank-local transforms plus one
+// all-to-all, every MSM over a per-rank slice of the SRS (DESIGN.md §6). The W ranks run as
+// concurrent async jobs on the libuv pool and all produce the same proof; rank 0 also returns the
+// Montgomery write-back. One sharded proof at a time (the group's barriers join the ranks of one
+// proof); the same inputs and the same Promise result as the single-GPU path.
+const shard = { ctxs: null, group: null, busy: Promise.resolve() };
+function shardRanks() {
+    const v = parseInt(process.env.KGS_JS_SHARD_RANKS || "0", 10);
+    return Number.isFinite(v) ? v : 0;
+}
+function shardMinBits() {
+    const v = parseInt(process.env.KGS_JS_SHARD_MIN_NBITS || "22", 10);
+    return Number.isFinite(v) ? v : 22;
+}
+function proveSharded(kind, key, nBits, evalsF, evalsT, selF, selT) {
+    const a = load();
+    const W = shardRanks();
+    const run = async () => {
+        if (!shard.ctxs || shard.ctxs.length !== W) {
+            const devs = devices();
+            shard.ctxs = Array.from({ length: W }, (_, r) => a.ctxCreate(devs[r % devs.length]));
+            shard.group = null;
+        }
+        if (!shard.group) {
+            shard.group = a.groupCreateLocal(W);
+            shard.ctxs.forEach((c, r) => a.ctxSetGroup(c, shard.group, r));
+        }
+        await Promise.all(shard.ctxs.map(c => a.srsLoadPtau(c, key, nBits)));
+        try {
+            const res = await Promise.all(shard.ctxs.map((c, r) =>
+                a.prove(c, kind, nBits, evalsF, evalsT, selF, selT, r === 0)));
+            return res[0];
+        } catch (e) {
+            // a rank failed: the group may be spent (the others were released with an error); make a
+            // fresh one for the next proof
+            shard.ctxs.forEach(c => a.ctxSetGroup(c, null, 0));
+            shard.group = null;
+            throw e;
+        }
+    };
+    const p = shard.busy.then(run, run);
+    shard.busy = p.catch(() => {});
+    return p;
 }
 
 function poolInfo() {

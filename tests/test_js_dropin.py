@@ -189,3 +189,40 @@ getCurveFromName('bn128').then(async c => {{
 }});
 """
     assert bytes.fromhex(_node_json(script)["r"]) == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_js_sharded_prover_matches_oracle(tmp_path, ranks):
+    """KGS_JS_SHARD_RANKS: the drop-in module proves one proof over `ranks` contexts joined by an
+    in-process rank group (every vector sharded; here all ranks on the one GPU of the box), through
+    the unchanged prover() API — byte-identical to the oracle, Montgomery write-back included, and
+    the reference's error message from a failing proof (the next proof still works)."""
+    ptau = common.oracle_ptau(9)
+    srs = P.SRS(ptau, common.tau())
+    cases, expect = [], []
+    for i, (kind, npols, sel, nbits) in enumerate((("grandsum", 1, False, 6), ("grandproduct", 2, True, 7),
+                                                   ("grandsum", 2, True, 8))):
+        Fs, Ts, sF, sT = common.make_inputs(8100 + i, nbits, npols, sel)
+        cases.append({"kind": kind, "F": [x.hex() for x in Fs], "T": [x.hex() for x in Ts],
+                      "selF": sF.hex() if sF else None, "selT": sT.hex() if sT else None})
+        eF = [P.EvalBuffer(x) for x in Fs]
+        eT = [P.EvalBuffer(x) for x in Ts]
+        pr = P.prove(kind, srs, eF if npols > 1 else eF[0], eT if npols > 1 else eT[0],
+                     P.EvalBuffer(sF) if sF else None, P.EvalBuffer(sT) if sT else None)
+        expect.append(({sec: {k: v.hex() for k, v in pr[sec].items()} for sec in ("commitments", "evaluations")},
+                       [e.eval.hex() for e in eF]))
+    Fs, _, _, _ = common.make_inputs(1, 6, 1, False)
+    F2, _, _, _ = common.make_inputs(2, 6, 1, False)
+    cases.insert(1, {"kind": "grandsum", "F": [Fs[0].hex()], "T": [F2[0].hex()], "selF": None, "selT": None})
+    spec = tmp_path / "spec.json"
+    spec.write_text(json.dumps({"ptau": ptau, "cases": cases}))
+    env = dict(os.environ, KGS_JS_SHARD_RANKS=str(ranks), KGS_JS_SHARD_MIN_NBITS="5")
+    out = json.loads(subprocess.check_output([NODE, os.path.join(JS, "test", "prove_from_json.js"), str(spec)],
+                                             timeout=600, env=env))
+    got = out["proofs"]
+    assert got[1]["error"] == "The grand-sum polynomial S is not well calculated"
+    for g, (exp, mont) in zip([got[0]] + got[2:], expect):
+        assert "error" not in g, g
+        assert {"commitments": g["commitments"], "evaluations": g["evaluations"]} == exp
+        assert g["montF"] == mont
