@@ -42,6 +42,15 @@ extern "C" {
 
 #define KGS_GRANDSUM 0
 #define KGS_GRANDPRODUCT 1
+/* Lookup (the commented-out cases of test/lookup_kzg_grandsum.test.js:24-44):
+ * the selected grand-sum with sel_t carrying MULTIPLICITIES, so that
+ *   sum_i selF_i / (f_i + gamma) == sum_i m_i / (t_i + gamma)
+ * (f's selected values all occur in t). Identical to KGS_GRANDSUM with selectors in every respect
+ * (transcript, proof layout, builder, error strings) except that the quotient and r(X) drop the
+ * binary constraint on sel_t (the alpha^3 (selT - selT^2) term of prover.js:241-244 and
+ * verifier.js:80-81). sel_f stays binary. Needs both selectors. Not in the reference, so parity is
+ * against the oracle's restatement only. */
+#define KGS_LOOKUP 2
 
 typedef struct kgs_ctx kgs_ctx_t;
 
@@ -133,7 +142,7 @@ int kgs_ptau_write_synthetic(kgs_ctx_t* ctx, const char* path, int power, const 
 
 /* Full prover — replaces mset_eq_kzg_{grandsum,grandproduct}_prover
  * (src/grandsum/mset_eq_kzg_prover.js:12, src/grandproduct/mset_eq_kzg_prover.js:12).
- *   kind      KGS_GRANDSUM | KGS_GRANDPRODUCT
+ *   kind      KGS_GRANDSUM | KGS_GRANDPRODUCT | KGS_LOOKUP (grand-sum layout; selectors required)
  *   nbits     domain size n = 2^nbits (1 <= nbits <= SRS nbits_max)
  *   npols     k >= 1 (vector argument when k > 1)
  *   evals_f/t k host pointers, n x 32 B STANDARD-form evaluations each (the caller's
@@ -162,7 +171,8 @@ int kgs_proof_shape(int kind, int npols, int selected, int* n_commitments, int* 
 /* ---- verifiers (host only; no context, no GPU) -------------------------------------------
  * mset_eq_kzg_grandsum_verifier / mset_eq_kzg_grandproduct_verifier
  * (src/grandsum/mset_eq_kzg_verifier.js:9, src/grandproduct/mset_eq_kzg_verifier.js:9): commitment
- * and evaluation buffers in the fixed order kgs_prove writes (kgs_proof_shape); tau_g2 = [tau]_2 as
+ * and evaluation buffers in the fixed order kgs_prove writes (kgs_proof_shape; KGS_LOOKUP proofs
+ * are checked with kind KGS_LOOKUP and selected = 1); tau_g2 = [tau]_2 as
  * 128 B LEM (the second point of ptau section 3, kgs_ptau_read_tau_g2). Returns 1 (valid), 0
  * (invalid: not on G1, evaluation >= r, or the pairing equation fails) or a negative error. */
 int kgs_verify(int kind, int nbits, int npols, int selected, const uint8_t* commitments, const uint8_t* evaluations,

@@ -5,6 +5,8 @@ Python mirror of the reference's module API (xavi-pinsach/kzg-grandsums-study):
     prover(pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None) -> proof
         src/grandsum/mset_eq_kzg_prover.js:12  -> grandsum_prover
         src/grandproduct/mset_eq_kzg_prover.js:12 -> grandproduct_prover
+    lookup_prover(pTauFilename, evalsFs, evalsTs, evalsSelF, evalsMulT) -> proof
+        test/lookup_kzg_grandsum.test.js:24-44 (commented out in the reference) -> KGS_LOOKUP
 
 over the C-ABI library lib/libkgs.so (include/kgs.h; HIP kernels for gfx950). The JavaScript
 drop-in modules (js/) bind the same library through an N-API addon. There is NO CPU fallback:
@@ -23,6 +25,7 @@ LIB_PATH = os.environ.get("KGS_LIB") or os.path.join(_HERE, "lib", "libkgs.so")
 
 GRANDSUM = 0
 GRANDPRODUCT = 1
+LOOKUP = 2
 
 R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 FR_ONE_MONT = ((1 << 256) % R).to_bytes(32, "little")
@@ -469,7 +472,7 @@ class Context:
 def proof_names(kind, npols, selected):
     """Commitment / evaluation key order of the C-ABI outputs (kgs.h) in the reference's names."""
     vec = npols > 1
-    gs = kind == GRANDSUM
+    gs = kind != GRANDPRODUCT
     com = []
     for i in range(npols):
         com += [f"F{i}" if vec else "F", f"T{i}" if vec else "T"]
@@ -515,6 +518,8 @@ def _prover(kind, pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None
         elif evalsFs[i].length() != evalsFs[0].length():
             raise ValueError("The multiset buffers must all have the same length.")
     n0 = evalsFs[0].length()
+    if kind == LOOKUP and evalsSelT is None:
+        raise ValueError("A lookup needs the multiplicities of the table.")
     if evalsSelF is None:
         evalsSelF = Evaluations.getOneEvals(n0)
     if evalsSelT is None:
@@ -523,7 +528,8 @@ def _prover(kind, pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None
         raise ValueError("The selection buffers must have the same length.")
     elif evalsSelF.length() != n0:
         raise ValueError("The selection buffers must have the same length as the multiset buffers.")
-    is_selected = not (evalsSelF.isAllOnes() and evalsSelT.isAllOnes())
+    # a lookup keeps its selectors even when all one (its proof always carries selF / selT)
+    is_selected = kind == LOOKUP or not (evalsSelF.isAllOnes() and evalsSelT.isAllOnes())
     nbits = (n0 - 1).bit_length() if n0 > 0 else 0
     if n0 != (1 << nbits):
         raise ValueError("Polynomial length must be a power of two.")
@@ -567,6 +573,8 @@ def _verifier(kind, pTauFilename, proof, nBits):
     nfi = len([k for k in keys if re.match(r"^F\d", k)])
     npols = nfi if nfi > 0 else 1
     selected = len([k for k in keys if re.match(r"^selF", k)]) == 1
+    if kind == LOOKUP and not selected:
+        return False
     cn, en = proof_names(kind, npols, selected)
     try:
         com = b"".join(bytes(proof["commitments"][n]) for n in cn)
@@ -588,3 +596,21 @@ def grandsum_verifier(pTauFilename, proof, nBits):
 def grandproduct_verifier(pTauFilename, proof, nBits):
     """mset_eq_kzg_grandproduct_verifier (src/grandproduct/mset_eq_kzg_verifier.js:9)."""
     return _verifier(GRANDPRODUCT, pTauFilename, proof, nBits)
+
+
+def lookup_prover(pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsMulT=None, device=0):
+    """Lookup argument: every selected f row (evalsSelF, binary; all ones if None)
+    is a row of the table t, and evalsMulT (Montgomery, required) holds how often each table row is
+    looked up. The commented-out cases of test/lookup_kzg_grandsum.test.js:24-44 call the grand-sum
+    prover with these arguments; this is that prover without the binary constraint on the
+    multiplicities (include/kgs.h KGS_LOOKUP). Same proof layout as a selected grand-sum."""
+    try:
+        return _prover(LOOKUP, pTauFilename, evalsFs, evalsTs, evalsSelF, evalsMulT, device)
+    except KgsError as e:
+        raise ValueError(str(e)) from e
+
+
+def lookup_verifier(pTauFilename, proof, nBits):
+    """Verifier of lookup_prover's proofs: the grand-sum verifier (src/grandsum/mset_eq_kzg_verifier.js:9)
+    without the selT-binary term of r0 (:80-81)."""
+    return _verifier(LOOKUP, pTauFilename, proof, nBits)

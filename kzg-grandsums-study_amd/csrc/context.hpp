@@ -357,7 +357,7 @@ struct R5 {
 };
 R5 round5_terms(bool gs, bool sel, int k, int nbits, const Fr& alpha, const Fr& beta, const Fr& gamma, const Fr& v,
                 const Fr& xi, const std::vector<Fr>& fx, const std::vector<Fr>& tx, const Fr& sFx, const Fr& sTx,
-                const Fr& sxiw);
+                const Fr& sxiw, bool lookup);
 
 void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out);
 // the distributed prover (prover_dist.cpp): same inputs and outputs as prove_impl on every rank

@@ -204,7 +204,7 @@ void launch_e_heads(hipStream_t st, uint32_t* heads, const uint32_t* S, uint64_t
 }
 
 // quotient on E-distributed coset evaluations (natural order inside each block). Scalars: alpha,
-// gamma, zinv0, zinv1. S(w x_i) = S[i + rot]: the same block at p + rot, or halo[k1 rot + ...] (the
+// gamma, zinv0, zinv1, alpha_t (selected only). S(w x_i) = S[i + rot]: the same block at p + rot, or halo[k1 rot + ...] (the
 // next chunk's first elements) past the block's end. nxm1[p] = 1/(n (x_i - 1)).
 template <bool PROD, bool SEL>
 __global__ void __launch_bounds__(256) k_quotient_e(uint32_t* __restrict__ q, const uint32_t* __restrict__ S,
@@ -222,7 +222,8 @@ __global__ void __launch_bounds__(256) k_quotient_e(uint32_t* __restrict__ q, co
   const fr s = fr::load(S + 8 * p);
   const fr sw = t + rot < b ? fr::load(S + 8 * (p + rot)) : fr::load(halo + 8 * (k1 * rot + (t + rot - b)));
   const fr sf = SEL ? fr::load(SF + 8 * p) : fr::zero(), st = SEL ? fr::load(ST + 8 * p) : fr::zero();
-  fr acc = quotient_core<PROD, SEL>(s, sw, fr::load(F + 8 * p), fr::load(T + 8 * p), sf, st, alpha, gamma);
+  fr acc = quotient_core<PROD, SEL>(s, sw, fr::load(F + 8 * p), fr::load(T + 8 * p), sf, st, alpha, gamma,
+                                            SEL ? fr::load(sc + 32) : fr::zero());
   const fr zinv = (rot == 2 && (gi & 1)) ? z1 : z0;
   acc = acc * zinv + quotient_l1<PROD>(s, fr::load(nxm1 + 8 * p));
   acc.store(q + 8 * p);

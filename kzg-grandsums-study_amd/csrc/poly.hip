@@ -362,14 +362,15 @@ __global__ void __launch_bounds__(256) k_quotient(uint32_t* __restrict__ q, cons
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t cs = 1ull << lcs;
   if (p >= cs) return;
-  // scalars: alpha, gamma, zinv0, zinv1
+  // scalars: alpha, gamma, zinv0, zinv1, alpha_t (selected only)
   const fr alpha = fr::load(sc), gamma = fr::load(sc + 8), z0 = fr::load(sc + 16), z1 = fr::load(sc + 24);
   const uint32_t i = brev((uint32_t)p, lcs);
   const uint32_t j = (i + rot) & (uint32_t)(cs - 1);
   const uint32_t pj = brev(j, lcs);
   const fr s = fr::load(S + 8 * p), sw = fr::load(S + 8 * (uint64_t)pj);
   const fr sf = SEL ? fr::load(SF + 8 * p) : fr::zero(), st = SEL ? fr::load(ST + 8 * p) : fr::zero();
-  fr acc = quotient_core<PROD, SEL>(s, sw, fr::load(F + 8 * p), fr::load(T + 8 * p), sf, st, alpha, gamma);
+  fr acc = quotient_core<PROD, SEL>(s, sw, fr::load(F + 8 * p), fr::load(T + 8 * p), sf, st, alpha, gamma,
+                                            SEL ? fr::load(sc + 32) : fr::zero());
   const fr zinv = (rot == 2 && (i & 1)) ? z1 : z0;
   acc = acc * zinv + quotient_l1<PROD>(s, fr::load(inv_nxm1 + 8 * p));
   acc.store(q + 8 * p);
@@ -403,7 +404,8 @@ __global__ void k_divcheck(uint32_t* __restrict__ flag, const uint32_t* __restri
   const fr alpha = fr::load(sc), gamma = fr::load(sc + 8);
   const fr s = fr::load(S + 8 * i), sw = i + 1 == n ? fr::load(S_next) : fr::load(S + 8 * (i + 1));
   const fr sf = SEL ? fr::load(sfp + 8 * i) : fr::zero(), st = SEL ? fr::load(stp + 8 * i) : fr::zero();
-  fr acc = quotient_core<PROD, SEL>(s, sw, fr::load(f + 8 * i), fr::load(t + 8 * i), sf, st, alpha, gamma);
+  fr acc = quotient_core<PROD, SEL>(s, sw, fr::load(f + 8 * i), fr::load(t + 8 * i), sf, st, alpha, gamma,
+                                            SEL ? fr::load(sc + 32) : fr::zero());
   if (gbase + i == 0) acc = acc + (PROD ? s - fr::one() : s);  // L1(w^0) = 1
   if (!acc.is_zero()) atomicOr(flag, 1u);
 }

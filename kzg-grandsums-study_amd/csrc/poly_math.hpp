@@ -3,6 +3,8 @@
 // Grand-sum (prover.js:233-286):
 //   N(x) = alpha [ (S(wx) - S(x)) (F+g)(T+g) + (T+g) selF - (F+g) selT ]  (unselected: + F - T)
 //          + alpha^2 (selF - selF^2) + alpha^3 (selT - selT^2)  + L1(x) S(x)
+// The selT-binary term is weighted by alpha_t = alpha (grand-sum) or 0 (KGS_LOOKUP: selT carries
+// multiplicities), so both arguments share one kernel and the grand-sum values are unchanged.
 // Grand-product (grandproduct prover.js:233-286): alpha [ Z(wx) dT - Z(x) dF ] + ... + L1(x) (Z(x) - 1)
 #pragma once
 #include "field.hpp"
@@ -12,12 +14,13 @@ namespace kgs {
 // alpha * (sel terms + main term); L1 part added by the caller
 template <bool PROD, bool SEL>
 __device__ __forceinline__ fr quotient_core(const fr& s, const fr& sw, const fr& fv, const fr& tv, const fr& sf,
-                                            const fr& st, const fr& alpha, const fr& gamma) {
+                                            const fr& st, const fr& alpha, const fr& gamma,
+                                            const fr& alpha_t) {
   const fr fg = fv + gamma, tg = tv + gamma;
   fr acc = fr::zero();
   if (SEL) {
     // alpha^3 (selT - selT^2) + alpha^2 (selF - selF^2)  ==  ((selT-selT^2)*alpha + (selF-selF^2))*alpha^2
-    acc = (st - st.sqr()) * alpha + (sf - sf.sqr());
+    acc = (st - st.sqr()) * alpha_t + (sf - sf.sqr());
     acc = acc * alpha;  // multiplied by alpha once more below together with the main term
   }
   fr q1;

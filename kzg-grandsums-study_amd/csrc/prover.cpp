@@ -460,7 +460,7 @@ void run_lincomb(hipStream_t st, uint32_t* out, uint64_t n, const LcTerms& t) {
 // single-GPU and the distributed prover.
 R5 round5_terms(bool gs, bool sel, int k, int nbits, const Fr& alpha, const Fr& beta, const Fr& gamma, const Fr& v,
                 const Fr& xi, const std::vector<Fr>& fx, const std::vector<Fr>& tx, const Fr& sFx, const Fr& sTx,
-                const Fr& sxiw) {
+                const Fr& sxiw, bool lookup) {
   const uint64_t n = 1ull << nbits;
   Fr xn = xi;
   for (int i = 0; i < nbits; i++) xn = xn.sqr();
@@ -472,8 +472,8 @@ R5 round5_terms(bool gs, bool sel, int k, int nbits, const Fr& alpha, const Fr& 
     if (gs) txi = txi * beta + tx[i];
   }
   const Fr one = Fr::one();
-  Fr selBin = Fr::zero();  // alpha^3 selTBin + alpha^2 selFBin
-  if (sel) selBin = ((sTx - sTx.sqr()) * alpha + (sFx - sFx.sqr())) * alpha * alpha;
+  Fr selBin = Fr::zero();  // alpha^3 selTBin + alpha^2 selFBin (a lookup has no selTBin term)
+  if (sel) selBin = ((lookup ? Fr::zero() : (sTx - sTx.sqr()) * alpha) + (sFx - sFx.sqr())) * alpha * alpha;
   std::vector<Fr> vp(2 * k + 4);
   vp[0] = one;
   for (size_t i = 1; i < vp.size(); i++) vp[i] = vp[i - 1] * v;
@@ -520,6 +520,10 @@ R5 round5_terms(bool gs, bool sel, int k, int nbits, const Fr& alpha, const Fr& 
 }
 
 void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out) {
+  if (in.kind != KGS_GRANDSUM && in.kind != KGS_GRANDPRODUCT && in.kind != KGS_LOOKUP)
+    throw KgsError(KGS_E_ARG, "unknown argument kind");
+  if (in.kind == KGS_LOOKUP && !in.sel_f)
+    throw KgsError(KGS_E_ARG, "a lookup needs both selectors (sel_t holds the multiplicities)");
   if (c.group) {
     prove_dist_group(c, in, com_out, ev_out);
     return;
@@ -536,7 +540,8 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     if (r + 1 < 5) range.push(ROUND_NAMES[r + 1]);
     else range.pop();
   };
-  const bool gs = in.kind == KGS_GRANDSUM;
+  const bool gs = in.kind != KGS_GRANDPRODUCT;  // KGS_LOOKUP is a selected grand-sum
+  const bool lk = in.kind == KGS_LOOKUP;
   const bool sel = in.sel_f != nullptr;
   const int k = in.npols;
   const int nbits = in.nbits;
@@ -704,8 +709,9 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   const uint32_t rot = (uint32_t)(cs >> nbits);
   const uint64_t qlen = (!gs && !sel) ? n - 1 : 2 * n - 2;  // deg Q + 1 bound
   Fr gn = Fr::from_u64(5).pow_u64(n);
-  Fr qs[4] = {alpha, gamma, (gn - Fr::one()).inverse(), (gn.neg() - Fr::one()).inverse()};
-  uint32_t* d_qs = c.scal(qs, 4);
+  // alpha_t: weight of the selT-binary term (none for a lookup, whose selT holds multiplicities)
+  Fr qs[5] = {alpha, gamma, (gn - Fr::one()).inverse(), (gn.neg() - Fr::one()).inverse(), lk ? Fr::zero() : alpha};
+  uint32_t* d_qs = c.scal(qs, 5);
   launch_divcheck(c.st, !gs, sel, flags + 1, Sev, fcomb, tcomb, in.sel_f, in.sel_t, d_qs, n);
   uint32_t* Qc = c.buf("Qc", 32 * cs);
   launch_quotient(c.st, !gs, sel, Qc, cosS, cosF, cosT, cosSF, cosST, nxm1, d_qs, lcs, rot);
@@ -781,7 +787,7 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   }
   tr.add_scalar(sxiw);
   const Fr v = tr.challenge();
-  const R5 r5 = round5_terms(gs, sel, k, nbits, alpha, beta, gamma, v, xi, fx, tx, sFx, sTx, sxiw);
+  const R5 r5 = round5_terms(gs, sel, k, nbits, alpha, beta, gamma, v, xi, fx, tx, sFx, sTx, sxiw, lk);
   LcTerms lw;
   for (const R5Term& t : r5.terms) {
     switch (t.id) {
@@ -1314,7 +1320,7 @@ int kgs_grand_build(kgs_ctx_t* ctx, int kind, const uint8_t* f_mont, const uint8
   bool bad = hf[0] != 0;
   ctx->reset_staging();
   if (bad)
-    throw KgsError(KGS_E_NOT_WELL_CALC, kind == KGS_GRANDSUM ? "The grand-sum polynomial S is not well calculated"
+    throw KgsError(KGS_E_NOT_WELL_CALC, kind != KGS_GRANDPRODUCT ? "The grand-sum polynomial S is not well calculated"
                                                              : "The grand-product polynomial Z is not well calculated");
   API_END
 }

@@ -283,7 +283,8 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
   };
   Dist D(c);
   const int W = D.W, r = D.r, logW = D.logW;
-  const bool gs = in.kind == KGS_GRANDSUM;
+  const bool gs = in.kind != KGS_GRANDPRODUCT;  // KGS_LOOKUP is a selected grand-sum
+  const bool lk = in.kind == KGS_LOOKUP;
   const bool sel = in.sel_f != nullptr;
   const int k = in.npols;
   const int nbits = in.nbits;
@@ -488,8 +489,9 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
   const uint32_t rot = (uint32_t)(cs >> nbits);
   const uint64_t qlen = (!gs && !sel) ? n - 1 : 2 * n - 2;  // deg Q + 1 bound
   Fr gn = Fr::from_u64(5).pow_u64(n);
-  Fr qs[4] = {alpha, gamma, (gn - Fr::one()).inverse(), (gn.neg() - Fr::one()).inverse()};
-  uint32_t* d_qs = c.scal(qs, 4);
+  // alpha_t: weight of the selT-binary term (none for a lookup, whose selT holds multiplicities)
+  Fr qs[5] = {alpha, gamma, (gn - Fr::one()).inverse(), (gn.neg() - Fr::one()).inverse(), lk ? Fr::zero() : alpha};
+  uint32_t* d_qs = c.scal(qs, 5);
   // divisibility on H (BLOCK): S at the next natural index past this block is d_offs[1]
   launch_divcheck(c.st, !gs, sel, flags + 1, SB, fcomb, tcomb, sFB, sTB, d_qs, M, d_offs + 8, (uint64_t)r * M);
   // quotient halo: the first rot coset values of the chunk following each of this rank's blocks
@@ -598,7 +600,7 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
   }
   tr.add_scalar(sxiw);
   const Fr v = tr.challenge();
-  const R5 r5 = round5_terms(gs, sel, k, nbits, alpha, beta, gamma, v, xi, fx, tx, sFx, sTx, sxiw);
+  const R5 r5 = round5_terms(gs, sel, k, nbits, alpha, beta, gamma, v, xi, fx, tx, sFx, sTx, sxiw, lk);
   const uint64_t qcnt = qlen > (uint64_t)r ? (qlen - r + W - 1) / W : 0;
   LcTerms lw;
   for (const R5Term& t : r5.terms) {

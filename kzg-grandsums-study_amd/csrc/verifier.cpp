@@ -49,6 +49,7 @@ struct Proof {
   bool sel, gs;
   const uint8_t* com;  // fixed order (kgs_proof_shape)
   const uint8_t* ev;
+  bool lookup = false;  // KGS_LOOKUP: no binary constraint on selT
   // commitment indices
   const uint8_t* F(int i) const { return com + 64 * (2 * i); }
   const uint8_t* T(int i) const { return com + 64 * (2 * i + 1); }
@@ -133,7 +134,8 @@ bool verify_impl(const Proof& p, int nbits, const host::G2A& tau_g2) {
   if (p.sel) {
     selF = fr_at(p.selFxi_raw());
     selT = fr_at(p.selTxi_raw());
-    r0 = (r0 + (selT - selT.sqr())) * alpha;
+    if (!p.lookup) r0 = r0 + (selT - selT.sqr());  // a lookup's selT holds multiplicities
+    r0 = r0 * alpha;
     r0 = (r0 + (selF - selF.sqr())) * alpha;
   }
   Fr fxi = Fr::zero(), txi = Fr::zero();
@@ -210,17 +212,19 @@ extern "C" {
 int kgs_proof_shape(int kind, int npols, int selected, int* n_commitments, int* n_evaluations) {
   if (npols < 1 || npols > (1 << 20)) return KGS_E_ARG;
   if (n_commitments) *n_commitments = 2 * npols + (selected ? 2 : 0) + 4;
-  if (n_evaluations) *n_evaluations = (kind == KGS_GRANDSUM ? 2 : 1) * npols + (selected ? 2 : 0) + 1;
+  if (kind != KGS_GRANDSUM && kind != KGS_GRANDPRODUCT && kind != KGS_LOOKUP) return KGS_E_ARG;
+  if (n_evaluations) *n_evaluations = (kind != KGS_GRANDPRODUCT ? 2 : 1) * npols + (selected ? 2 : 0) + 1;
   return KGS_OK;
 }
 
 int kgs_verify(int kind, int nbits, int npols, int selected, const uint8_t* commitments, const uint8_t* evaluations,
                const uint8_t tau_g2[128]) {
-  if ((kind != KGS_GRANDSUM && kind != KGS_GRANDPRODUCT) || nbits < 1 || nbits > 28 || npols < 1 || !commitments ||
+  if ((kind != KGS_GRANDSUM && kind != KGS_GRANDPRODUCT && kind != KGS_LOOKUP) || (kind == KGS_LOOKUP && !selected) ||
+      nbits < 1 || nbits > 28 || npols < 1 || !commitments ||
       !evaluations || !tau_g2)
     return KGS_E_ARG;
   try {
-    Proof p{npols, selected != 0, kind == KGS_GRANDSUM, commitments, evaluations};
+    Proof p{npols, selected != 0, kind != KGS_GRANDPRODUCT, commitments, evaluations, kind == KGS_LOOKUP};
     host::G2A t2 = host::g2_from_lem(tau_g2);
     if (!host::g2_on_curve(t2)) return KGS_E_ARG;
     return verify_impl(p, nbits, t2) ? 1 : 0;

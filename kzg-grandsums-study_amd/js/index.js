@@ -6,4 +6,6 @@ module.exports = {
     mset_eq_kzg_grandproduct_prover: require("./src/grandproduct/mset_eq_kzg_prover"),
     mset_eq_kzg_grandsum_verifier: require("./src/grandsum/mset_eq_kzg_verifier"),
     mset_eq_kzg_grandproduct_verifier: require("./src/grandproduct/mset_eq_kzg_verifier"),
+    lookup_kzg_grandsum_prover: require("./src/lookup/lookup_kzg_prover"),
+    lookup_kzg_grandsum_verifier: require("./src/lookup/lookup_kzg_verifier"),
 };

@@ -144,4 +144,4 @@ function poolInfo() {
              idle: pool.idle.length, waiting: pool.waiters.length };
 }
 
-module.exports = { load, ptauPower, prove, withContext, poolInfo, GRANDSUM: 0, GRANDPRODUCT: 1 };
+module.exports = { load, ptauPower, prove, withContext, poolInfo, GRANDSUM: 0, GRANDPRODUCT: 1, LOOKUP: 2 };

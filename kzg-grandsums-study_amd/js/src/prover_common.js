@@ -1,4 +1,4 @@
-// Shared body of the two drop-in provers: the reference's input checks (same messages,
+// Shared body of the drop-in provers (grand-sum, grand-product, lookup): the reference's input checks (same messages,
 // src/grandsum/mset_eq_kzg_prover.js:22-81), the HIP prover call, and the proof object with the
 // reference's key names and insertion order.
 const backend = require("./backend");
@@ -25,6 +25,8 @@ async function prove(kind, pTauFilename, evalsFs, evalsTs, evalsSelF, evalsSelT)
     // need not be materialised; given ones are checked with the same rules and messages
     const noSelF = evalsSelF === null || evalsSelF === undefined;
     const noSelT = evalsSelT === null || evalsSelT === undefined;
+    const isLookup = kind === backend.LOOKUP;
+    if (isLookup && noSelT) throw new Error("A lookup needs the multiplicities of the table.");
     const lenSelF = noSelF ? evalsFs[0].length() : evalsSelF.length();
     const lenSelT = noSelT ? evalsTs[0].length() : evalsSelT.length();
     if (lenSelF !== lenSelT) {
@@ -32,8 +34,9 @@ async function prove(kind, pTauFilename, evalsFs, evalsTs, evalsSelF, evalsSelT)
     } else if (lenSelF !== evalsFs[0].length()) {
         throw new Error("The selection buffers must have the same length as the multiset buffers.");
     }
+    // a lookup keeps its selectors even when all one (its proof always carries selF / selT)
     let isSelected = true;
-    if ((noSelF || evalsSelF.isAllOnes()) && (noSelT || evalsSelT.isAllOnes())) isSelected = false;
+    if (!isLookup && (noSelF || evalsSelF.isAllOnes()) && (noSelT || evalsSelT.isAllOnes())) isSelected = false;
     if (isSelected) {
         if (noSelF) evalsSelF = Evaluations.getOneEvals(lenSelF, curve);
         if (noSelT) evalsSelT = Evaluations.getOneEvals(lenSelT, curve);
@@ -51,7 +54,7 @@ async function prove(kind, pTauFilename, evalsFs, evalsTs, evalsSelF, evalsSelT)
         evalsTs[i].eval = res.montT[i];
     }
     const isVector = nPols > 1;
-    const gs = kind === backend.GRANDSUM;
+    const gs = kind !== backend.GRANDPRODUCT;
     const proof = { evaluations: {}, commitments: {} };
     let c = 0;
     for (let i = 0; i < nPols; i++) {

@@ -10,7 +10,8 @@ async function verify(kind, pTauFilename, proof, nBits) {
     const nPols = nFi > 0 ? nFi : 1;
     const isVector = nPols > 1;
     const isSelected = keys.filter(k => k.match(/^selF/)).length === 1;
-    const gs = kind === backend.GRANDSUM;
+    const gs = kind !== backend.GRANDPRODUCT;
+    if (kind === backend.LOOKUP && !isSelected) return false;
     const cNames = [], eNames = [];
     for (let i = 0; i < nPols; i++) {
         cNames.push(isVector ? `F${i}` : "F", isVector ? `T${i}` : "T");

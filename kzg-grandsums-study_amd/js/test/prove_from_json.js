@@ -3,7 +3,8 @@
 // With spec.concurrent every case is started at once (Promise.all), as independent reference calls
 // would be (src/grandsum/mset_eq_kzg_prover.js:12 is an independent async function per call).
 const fs = require("fs");
-const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_grandproduct_prover } = require("../index");
+const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_grandproduct_prover,
+        lookup_kzg_grandsum_prover } = require("../index");
 
 (async () => {
     const spec = JSON.parse(fs.readFileSync(process.argv[2], "utf8"));
@@ -12,7 +13,8 @@ const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_
     const ev = h => new Evaluations(new Uint8Array(Buffer.from(h, "hex")), curve);
     const one = async c => {
         const F = c.F.map(ev), T = c.T.map(ev);
-        const fn = c.kind === "grandsum" ? mset_eq_kzg_grandsum_prover : mset_eq_kzg_grandproduct_prover;
+        const fn = { grandsum: mset_eq_kzg_grandsum_prover, grandproduct: mset_eq_kzg_grandproduct_prover,
+                     lookup: lookup_kzg_grandsum_prover }[c.kind];
         try {
             const proof = await fn(spec.ptau, F.length === 1 ? F[0] : F, T.length === 1 ? T[0] : T,
                 c.selF ? ev(c.selF) : null, c.selT ? ev(c.selT) : null);

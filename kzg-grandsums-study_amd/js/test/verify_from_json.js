@@ -1,7 +1,7 @@
 // Test driver used by tests/test_verifier.py: read {ptau, cases:[{kind, nbits, commitments:{k:hex},
 // evaluations:{k:hex}}]} from argv[2], run the drop-in verifiers, print {verdicts:[bool|string]}.
 const fs = require("fs");
-const { mset_eq_kzg_grandsum_verifier, mset_eq_kzg_grandproduct_verifier } = require("../index");
+const { mset_eq_kzg_grandsum_verifier, mset_eq_kzg_grandproduct_verifier, lookup_kzg_grandsum_verifier } = require("../index");
 
 (async () => {
     const spec = JSON.parse(fs.readFileSync(process.argv[2], "utf8"));
@@ -11,7 +11,8 @@ const { mset_eq_kzg_grandsum_verifier, mset_eq_kzg_grandproduct_verifier } = req
         const proof = { commitments: {}, evaluations: {} };
         for (const k of Object.keys(c.commitments)) proof.commitments[k] = u8(c.commitments[k]);
         for (const k of Object.keys(c.evaluations)) proof.evaluations[k] = u8(c.evaluations[k]);
-        const fn = c.kind === "grandsum" ? mset_eq_kzg_grandsum_verifier : mset_eq_kzg_grandproduct_verifier;
+        const fn = { grandsum: mset_eq_kzg_grandsum_verifier, grandproduct: mset_eq_kzg_grandproduct_verifier,
+                     lookup: lookup_kzg_grandsum_verifier }[c.kind];
         try {
             out.push(await fn(spec.ptau, proof, c.nbits));
         } catch (e) {

@@ -413,7 +413,8 @@ static fe tr_challenge(const transcript* t) {
 }
 
 /* ------------------------------------------------------------------ provers */
-/* kind 0 = grand-sum, 1 = grand-product. Outputs in the C-ABI order of include/kgs.h.
+/* kind 0 = grand-sum, 1 = grand-product, 2 = lookup (grand-sum with selt = multiplicities and no
+ * binary constraint on selt; selectors required). Outputs in the C-ABI order of include/kgs.h.
  * Returns 0 or -3 (not well calculated), -4 (not divisible), -5 (does not divide), -1 (args). */
 int orc_prove(int kind, int nbits, int npols, const uint8_t* const* f_std, const uint8_t* const* t_std,
               const uint8_t* self, const uint8_t* selt, const uint8_t* srs, uint64_t npts, int threads,
@@ -421,8 +422,9 @@ int orc_prove(int kind, int nbits, int npols, const uint8_t* const* f_std, const
 #ifdef _OPENMP
   if (threads > 0) omp_set_num_threads(threads);
 #endif
-  if (npols < 1 || nbits < 1) return -1;
-  const int gs = kind == 0, sel = self != NULL, vec = npols > 1;
+  if (npols < 1 || nbits < 1 || kind < 0 || kind > 2) return -1;
+  if (kind == 2 && (!self || !selt)) return -1;
+  const int gs = kind != 1, lk = kind == 2, sel = self != NULL, vec = npols > 1;
   const uint64_t n = 1ull << nbits;
   if (npts < 2 * n - 1) return -1;
   const fe one = f_one(&FR);
@@ -517,9 +519,13 @@ int orc_prove(int kind, int nbits, int npols, const uint8_t* const* f_std, const
   fe alpha = tr_challenge(&tr);
   poly polQ = p_new(n);
   if (sel) {
-    poly b1 = p_clone(&selT), b2 = p_clone(&selT); p_multiply(&b1, &b2);
-    poly sb = p_clone(&selT); p_addsub(&sb, &b1, 1); p_addsub(&polQ, &sb, 0); p_mul_scalar(&polQ, alpha);
-    p_free(&b1); p_free(&b2); p_free(&sb);
+    poly b1, b2, sb;
+    if (!lk) { /* prover.js:241-244 (a lookup's selT holds multiplicities) */
+      b1 = p_clone(&selT); b2 = p_clone(&selT); p_multiply(&b1, &b2);
+      sb = p_clone(&selT); p_addsub(&sb, &b1, 1); p_addsub(&polQ, &sb, 0);
+      p_free(&b1); p_free(&b2); p_free(&sb);
+    }
+    p_mul_scalar(&polQ, alpha);
     b1 = p_clone(&selF); b2 = p_clone(&selF); p_multiply(&b1, &b2);
     sb = p_clone(&selF); p_addsub(&sb, &b1, 1); p_addsub(&polQ, &sb, 0); p_mul_scalar(&polQ, alpha);
     p_free(&b1); p_free(&b2); p_free(&sb);
@@ -598,7 +604,8 @@ int orc_prove(int kind, int nbits, int npols, const uint8_t* const* f_std, const
   fe l1 = RM(zh, f_inv(&FR, RM(f_from_u64(&FR, n), RS(xi, one))));
   poly polR = p_new(n);
   if (sel) {
-    p_add_scalar(&polR, RS(sTx, RM(sTx, sTx))); p_mul_scalar(&polR, alpha);
+    if (!lk) p_add_scalar(&polR, RS(sTx, RM(sTx, sTx)));
+    p_mul_scalar(&polR, alpha);
     p_add_scalar(&polR, RS(sFx, RM(sFx, sFx))); p_mul_scalar(&polR, alpha);
   }
   fe fxi = p_eval(&polF, xi);

@@ -55,18 +55,19 @@ MESSAGES = {-3: None, -4: "Polynomial is not divisible", -5: "Polynomial does no
 
 
 def prove_raw(kind, nbits, Fs, Ts, sF, sT, srs_bytes, threads=0):
-    """kind 0/1; Fs/Ts lists of std bytes; sF/sT Montgomery bytes or None -> (coms, evs)."""
+    """kind 0/1/2 (grand-sum, grand-product, lookup); Fs/Ts lists of std bytes; sF/sT Montgomery
+    bytes or None -> (coms, evs)."""
     k = len(Fs)
     sel = sF is not None
     nc = 2 * k + (2 if sel else 0) + 4
-    ne = (2 if kind == 0 else 1) * k + (2 if sel else 0) + 1
+    ne = (2 if kind != 1 else 1) * k + (2 if sel else 0) + 1
     com = ctypes.create_string_buffer(64 * nc)
     ev = ctypes.create_string_buffer(32 * ne)
     FA = (ctypes.c_char_p * k)(*Fs)
     TA = (ctypes.c_char_p * k)(*Ts)
     rc = lib().orc_prove(kind, nbits, k, FA, TA, sF, sT, srs_bytes, len(srs_bytes) // 64, threads, com, ev)
     if rc == -3:
-        raise ValueError("The grand-sum polynomial S is not well calculated" if kind == 0
+        raise ValueError("The grand-sum polynomial S is not well calculated" if kind != 1
                          else "The grand-product polynomial Z is not well calculated")
     if rc:
         raise ValueError(MESSAGES.get(rc, f"oracle error {rc}"))

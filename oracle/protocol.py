@@ -111,8 +111,9 @@ def _as_list(x):
     return list(x) if isinstance(x, (list, tuple)) else [x]
 
 
-def _check_inputs(srs, evalsFs, evalsTs, selF, selT):
-    """mset_eq_kzg_prover.js:22-81 (same checks, same messages)."""
+def _check_inputs(srs, evalsFs, evalsTs, selF, selT, lookup=False):
+    """mset_eq_kzg_prover.js:22-81 (same checks, same messages). A lookup keeps its selectors
+    even when they are all one (its proof layout always has selF/selT)."""
     evalsFs = _as_list(evalsFs)
     evalsTs = _as_list(evalsTs)
     if len(evalsFs) != len(evalsTs):
@@ -126,6 +127,8 @@ def _check_inputs(srs, evalsFs, evalsTs, selF, selT):
         elif evalsFs[i].length() != evalsFs[0].length():
             raise ValueError("The multiset buffers must all have the same length.")
     n0 = evalsFs[0].length()
+    if lookup and selT is None:
+        raise ValueError("A lookup needs the multiplicities of the table.")
     if selF is None:
         selF = EvalBuffer(mont_bytes([1] * n0))
     if selT is None:
@@ -136,7 +139,7 @@ def _check_inputs(srs, evalsFs, evalsTs, selF, selT):
         raise ValueError("The selection buffers must have the same length as the multiset buffers.")
     selFv = selF.mont_values()
     selTv = selT.mont_values()
-    is_selected = not (all(v == 1 for v in selFv) and all(v == 1 for v in selTv))
+    is_selected = lookup or not (all(v == 1 for v in selFv) and all(v == 1 for v in selTv))
     nbits = (n0 - 1).bit_length()
     if n0 != 1 << nbits:
         raise ValueError("Polynomial length must be a power of two.")
@@ -188,11 +191,15 @@ def _grandproduct_Z(evF, evT, selF, selT, gamma):
 
 
 def prove(kind, srs, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, trace=None):
-    """kind in {"grandsum", "grandproduct"}; returns the proof dict (byte-level ffjs encoding)."""
-    assert kind in ("grandsum", "grandproduct")
-    gs = kind == "grandsum"
+    """kind in {"grandsum", "grandproduct", "lookup"}; returns the proof dict (byte-level ffjs
+    encoding). "lookup" (test/lookup_kzg_grandsum.test.js:24-44, commented out in
+    the reference, so this restatement is parity-unpinned): the selected grand-sum with evalsSelT
+    holding the table's multiplicities and no binary constraint on selT (prover.js:241-244 dropped)."""
+    assert kind in ("grandsum", "grandproduct", "lookup")
+    gs = kind != "grandproduct"
+    lookup = kind == "lookup"
     evalsFs, evalsTs, selFv, selTv, is_selected, nbits = _check_inputs(
-        srs, evalsFs, evalsTs, evalsSelF, evalsSelT)
+        srs, evalsFs, evalsTs, evalsSelF, evalsSelT, lookup)
     npols = len(evalsFs)
     n = 1 << nbits
     is_vector = npols > 1
@@ -266,9 +273,11 @@ def prove(kind, srs, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, trace=Non
     ch["alpha"] = alpha = tr.get_challenge()
     polQ = Polynomial.zero(n)
     if is_selected:
-        b1 = selT.clone()
-        b1.multiply(selT.clone())
-        polQ.add(selT.clone().sub(b1)).mul_scalar(alpha)
+        if not lookup:
+            b1 = selT.clone()
+            b1.multiply(selT.clone())
+            polQ.add(selT.clone().sub(b1))
+        polQ.mul_scalar(alpha)
         b1 = selF.clone()
         b1.multiply(selF.clone())
         polQ.add(selF.clone().sub(b1)).mul_scalar(alpha)
@@ -351,7 +360,7 @@ def prove(kind, srs, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, trace=Non
     if is_selected:
         sT = ev["selTxi"]
         sF = ev["selFxi"]
-        polR.add_scalar((sT - sT * sT) % R).mul_scalar(alpha)
+        polR.add_scalar(0 if lookup else (sT - sT * sT) % R).mul_scalar(alpha)
         polR.add_scalar((sF - sF * sF) % R).mul_scalar(alpha)
     fxi = polF.evaluate(xi)
     if gs:
@@ -420,7 +429,8 @@ def verify(kind, ptau, proof, nbits, tau=None):
     equivalent trapdoor test tau·A == B (same verdict, much faster); otherwise the restated
     optimal-ate pairing is used.
     """
-    gs = kind == "grandsum"
+    gs = kind != "grandproduct"
+    lookup = kind == "lookup"
     zname, ename = ("S", "sxiw") if gs else ("Z", "zxiw")
     if not isinstance(ptau, PTau):
         ptau = PTau(ptau)
@@ -430,6 +440,8 @@ def verify(kind, ptau, proof, nbits, tau=None):
     npols = nF if nF > 0 else 1
     is_vector = npols > 1
     is_selected = "selF" in com
+    if lookup and not is_selected:
+        return False
     # validateCommitments / validateEvaluations (verifier.js:194-244)
     for k, p in com.items():
         if not bn.g1_is_on_curve(p):
@@ -483,7 +495,7 @@ def verify(kind, ptau, proof, nbits, tau=None):
     r0 = 0
     if is_selected:
         sT, sF = ev["selTxi"], ev["selFxi"]
-        r0 = (r0 + sT - sT * sT) * alpha % R
+        r0 = (r0 + (0 if lookup else sT - sT * sT)) * alpha % R
         r0 = (r0 + sF - sF * sF) * alpha % R
     fxi = 0
     txi = 0

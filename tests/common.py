@@ -60,6 +60,40 @@ def make_inputs(seed, nbits, npols, selected):
     return Fs, Ts, sF, sT
 
 
+def make_lookup_inputs(seed, nbits, npols, unselected=0):
+    """Lookup inputs (test/lookup_kzg_grandsum.test.js:24-44 pattern, generalised): a random table T
+    (k columns), every F row a random table row, `unselected` F rows switched off in selF, and the
+    multiplicities m[j] = #selected F rows equal to table row j.
+    -> (F std-bytes list, T std-bytes list, selF mont-bytes, m mont-bytes)"""
+    rnd = random.Random(seed)
+    n = 1 << nbits
+    T = [[rnd.randrange(R) for _ in range(n)] for _ in range(npols)]
+    rows = [rnd.randrange(n) for _ in range(n)]
+    sel = [1] * n
+    for i in rnd.sample(range(n), unselected):
+        sel[i] = 0
+    m = [0] * n
+    for i in range(n):
+        m[rows[i]] += sel[i]
+    Fs = [std_bytes([T[c][rows[i]] for i in range(n)]) for c in range(npols)]
+    return Fs, [std_bytes(t) for t in T], mont_bytes(sel), mont_bytes(m)
+
+
+def reference_standard_lookup(seed=3, nbits=2):
+    """The reference's commented-out "standard lookup" case (test/lookup_kzg_grandsum.test.js:24-44):
+    T random, F = T with F[1] = F[n-1] = F[0], selF all ones, multiplicities one except m[0] = 3,
+    m[1] = m[n-1] = 0."""
+    rnd = random.Random(seed)
+    n = 1 << nbits
+    t = [rnd.randrange(R) for _ in range(n)]
+    f = list(t)
+    f[1] = f[0]
+    f[n - 1] = f[0]
+    m = [1] * n
+    m[0], m[1], m[n - 1] = 3, 0, 0
+    return [std_bytes(f)], [std_bytes(t)], mont_bytes([1] * n), mont_bytes(m)
+
+
 def inputs_digest(Fs, Ts, sF, sT):
     h = hashlib.sha256()
     for x in Fs + Ts + [sF or b"", sT or b""]:
