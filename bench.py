@@ -37,6 +37,7 @@ import importlib.util
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -245,6 +246,8 @@ def main():
     ap.add_argument("--c4-proofs", type=int, default=3)
     ap.add_argument("--sv-proofs", type=int, default=3,
                     help="proofs timed in the selected-vector leg (N > 1: MSMs sharded over all ranks)")
+    ap.add_argument("--legs-timeout", type=float, default=300.0,
+                    help="watchdog on the extra legs (seconds, 0 = none): on expiry the line is printed without them")
     ap.add_argument("--inflight", type=int, default=4,
                     help="independent proofs in flight per GPU (one context + HIP stream + host thread each)")
     args = ap.parse_args()
@@ -380,9 +383,143 @@ def main():
             except Exception as e:  # the JS leg must not hide the GPU number
                 host_leg["javascript_module"] = {"error": str(e)[:200]}
 
+    msm = roofline = hbm_view = cpu = None
+    extra_cfg = {}
+    if rank == 0:
+        log("MSM leg")
+        # ---------------- MSM leg: live HIP-event timing of the phases at N = n
+        sc = torch.from_numpy(synth_evals(n, 777)[0].reshape(-1).copy()).to(f"cuda:{local}")
+        phase = (ctypes.c_double * 4)()
+        entries = ctypes.c_uint64()
+        reps = args.msm_reps
+        K._check(K.lib().kgs_bench_msm_phases(ctx.handle, ctypes.c_void_p(sc.data_ptr()), n, reps, phase,
+                                              ctypes.byref(entries)))
+        ph = [phase[i] / reps for i in range(4)]
+        msm_ms = sum(ph)
+        W = (255 + window_c - 1) // window_c
+        B = 1 << (window_c - 1)
+        # executed G1 additions: one mixed add per (bucket, point) entry + combine (~ segments) +
+        # bit-sum trees (~ c * B / 2) + host Horner (2c)
+        adds_exec = entries.value + window_c * (B // 2) + 2 * window_c
+        msm = {
+            "n_points": n, "window_c": window_c, "windows": W, "precomputed_windows": True,
+            "ms": round(msm_ms, 4), "phase_ms": {"digits_sort": round(ph[0], 4), "accumulate": round(ph[1], 4),
+                                                 "combine": round(ph[2], 4), "reduce": round(ph[3], 4)},
+            "points_per_s": n / (msm_ms / 1e3),
+            "g1_adds_per_s_canonical_16N": 16 * n / (msm_ms / 1e3),
+            "g1_adds_executed": adds_exec,
+            "g1_adds_per_s_executed": adds_exec / (msm_ms / 1e3),
+        }
+
+        # ---------------- roofline of the dominant kernel (k_accumulate)
+        # The kernel is integer-VALU issue bound. Algorithmic work per launch: entries x 1 mixed XYZZ add
+        # (madd-2008-s: 8M + 2S = 10 Fq Montgomery products). Peak: the Fq-product rate at which the
+        # chip's measured v_mad_u64_u32 issue rate (MAD_PEAK: MAD_CYCLES SIMD cycles per wave64
+        # instruction at the 2.4 GHz nominal clock, profiles/ubench/) is spent on nothing but the mads of
+        # a product — no carries, loads or control: `peak` for the kernel's 9 x 29-bit product (162
+        # mads), `peak_8x32` for the 128 mads of 8 x 32-bit limbs (the fewest 32x32-bit partial products
+        # a 254-bit Montgomery product can have on this ISA). Timed with HIP events on the MSM's stream
+        # around the k_accumulate launch alone.
+        acc_ms = ph[1]
+        mults = 10 * entries.value
+        achieved = mults / (acc_ms / 1e3) / 1e9
+        peak = MAD_PEAK / MADS_PER_PRODUCT_29 / 1e9
+        peak32 = MAD_PEAK / MADS_PER_PRODUCT_32 / 1e9
+        traffic = None
+        pmc_path = os.path.join(HERE, "profiles", "pmc_accumulate.json")
+        if os.path.exists(pmc_path):
+            try:
+                with open(pmc_path) as fh:
+                    traffic = json.load(fh).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roofline = {"bound": "valu", "kernel": "k_accumulate", "achieved": round(achieved, 2), "peak": round(peak, 2),
+                    "unit": "G Fq-products/s", "frac": round(achieved / peak, 4),
+                    "peak_8x32": round(peak32, 2), "frac_8x32": round(achieved / peak32, 4), "traffic": traffic,
+                    "peak_note": f"v_mad_u64_u32 issue rate ({MAD_CYCLES} SIMD cycles per wave64 instruction, 256 CUs x 4 "
+                                 f"SIMDs, 2.4 GHz) / mads per product: 162 (9 x 29-bit, peak) or 128 (8 x 32-bit, peak_8x32)",
+                    "bound_note": "integer-VALU issue bound (254-bit Montgomery products on v_mad_u64_u32): neither the "
+                                  "HBM roof (the kernel moves ~1 TB/s of 8) nor MFMA (no dense contraction) applies",
+                    "mad_issue_frac": round(entries.value * MADS_PER_ADD / (acc_ms / 1e3) / MAD_PEAK, 4),
+                    "g1_adds_per_s": round(entries.value / (acc_ms / 1e3)),
+                    "algorithmic_bytes_per_launch": 68 * entries.value,
+                    "hbm_gbps_algorithmic": round(68 * entries.value / (acc_ms / 1e3) / 1e9, 1)}
+
+        # ---------------- proof-level HBM view (north star: achieved HBM-bandwidth fraction). Bytes per
+        # proof = SURVEY.md §8d's count over the REFERENCE op list, B_gs(n) = 131 E = 4192 n (grand-sum,
+        # k = 1, no selectors); the re-planned GPU path moves fewer, so this is an upper-bound view.
+        b_proof = (4192 if args.kind == "grandsum" else 101 * 32) * n
+        hbm_view = {"algorithmic_bytes_per_proof": b_proof, "achieved_GBps": round(b_proof * value / 1e9, 1),
+                    "peak_GBps": 8000.0, "frac": round(b_proof * value / 1e9 / 8000.0, 4),
+                    "accumulate_pmc_GBps": round(traffic / (acc_ms / 1e3) / 1e9, 1) if traffic else None,
+                    "note": "the proof is INT-VALU bound (MSM bucket accumulation), not HBM bound"}
+
+        # ---------------- CPU baseline (oracle/c port of the reference op list), N = 1 only
+        log("CPU baseline")
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                sys.path.insert(0, HERE)
+                from oracle import cbackend
+                cpu = cbackend.cpu_baseline(nbits, args.kind, threads=args.cpu_threads, ptau=ptau)
+            except Exception as e:  # baseline failure must not hide the GPU number
+                cpu = {"error": str(e)[:200]}
+
+
+    out = {
+        "metric": "grand-sum proofs/sec + MSM G1-adds/sec at n=2^20, 1/2/4/8 MI355X",
+        "value": round(value, 4),
+        "unit": "proofs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 limbs (BN254 Fr/Fq Montgomery: 8 x 32-bit; MSM buckets 9 x 29-bit), int VALU",
+        "data": "synthetic (PCG64-seeded multisets, T = rot(F); synthetic ptau, tau = keccak('kgs-bench-tau'))",
+        "config": {"workload": f"{args.kind} prover, n=2^{nbits}, k={args.npols}, no selectors, inputs resident in HBM",
+                   "nbits": nbits, "npols": args.npols, "selectors": False, "parallelism": f"replicas x{world}", "inflight_per_gpu": args.inflight,
+                   "srs_power": power, "srs_points_resident": npts, "srs_gen_s": round(t_gen, 2),
+                   "srs_load_s": round(t_load, 2)},
+        "proof_verified": proof_verified,
+        "host_buffer_boundary": host_leg,
+        "latency_ms_single_proof": round(latency_ms, 3),
+        "round_ms_single_proof": [round(x, 3) for x in rounds],
+        "msm": msm,
+        "roofline": roofline,
+        "hbm_view": hbm_view,
+        "extra_configs": extra_cfg,
+        "cpu_baseline": cpu,
+    }
+
+    # The extra legs run last, under a watchdog: at N > 1 they exercise the RCCL transport of the
+    # distributed prover, and a rank that hangs there must not cost the headline line. On expiry rank
+    # 0 prints the line with the legs measured so far and every rank exits.
+    emitted = threading.Lock()
+    state = {"printed": False}
+
+    def emit():
+        with emitted:
+            if rank == 0 and not state["printed"]:
+                print(json.dumps(dict(out, extra_configs=dict(extra_cfg))), flush=True)
+                state["printed"] = True
+
+    def legs_timeout():
+        extra_cfg["timeout"] = f"extra legs exceeded {args.legs_timeout} s; line emitted without the rest"
+        log(extra_cfg["timeout"])
+        emit()
+        sys.stdout.flush()
+        os._exit(0)
+
+    wd = None
+    if args.legs_timeout > 0:
+        wd = threading.Timer(args.legs_timeout + (0 if rank == 0 else 30), legs_timeout)
+        wd.daemon = True
+        wd.start()
     # ---------------- extra configs (BASELINE.json configs[2] and [4]), outside the timed region
     log("extra configs")
-    extra_cfg = {}
     if args.extra_legs:
         # C3: grand-product at the same n, same contexts / inputs (replicas per GPU)
         gp_steps = 4 * len(ctxs)
@@ -433,119 +570,9 @@ def main():
         if group is not None:
             group[0].close()
 
-    if rank != 0:
-        if dist:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
-
-    log("MSM leg")
-    # ---------------- MSM leg: live HIP-event timing of the phases at N = n
-    sc = torch.from_numpy(synth_evals(n, 777)[0].reshape(-1).copy()).to(f"cuda:{local}")
-    phase = (ctypes.c_double * 4)()
-    entries = ctypes.c_uint64()
-    reps = args.msm_reps
-    K._check(K.lib().kgs_bench_msm_phases(ctx.handle, ctypes.c_void_p(sc.data_ptr()), n, reps, phase,
-                                          ctypes.byref(entries)))
-    ph = [phase[i] / reps for i in range(4)]
-    msm_ms = sum(ph)
-    W = (255 + window_c - 1) // window_c
-    B = 1 << (window_c - 1)
-    # executed G1 additions: one mixed add per (bucket, point) entry + combine (~ segments) +
-    # bit-sum trees (~ c * B / 2) + host Horner (2c)
-    adds_exec = entries.value + window_c * (B // 2) + 2 * window_c
-    msm = {
-        "n_points": n, "window_c": window_c, "windows": W, "precomputed_windows": True,
-        "ms": round(msm_ms, 4), "phase_ms": {"digits_sort": round(ph[0], 4), "accumulate": round(ph[1], 4),
-                                             "combine": round(ph[2], 4), "reduce": round(ph[3], 4)},
-        "points_per_s": n / (msm_ms / 1e3),
-        "g1_adds_per_s_canonical_16N": 16 * n / (msm_ms / 1e3),
-        "g1_adds_executed": adds_exec,
-        "g1_adds_per_s_executed": adds_exec / (msm_ms / 1e3),
-    }
-
-    # ---------------- roofline of the dominant kernel (k_accumulate)
-    # The kernel is integer-VALU issue bound. Algorithmic work per launch: entries x 1 mixed XYZZ add
-    # (madd-2008-s: 8M + 2S = 10 Fq Montgomery products). Peak: the Fq-product rate at which the
-    # chip's measured v_mad_u64_u32 issue rate (MAD_PEAK: MAD_CYCLES SIMD cycles per wave64
-    # instruction at the 2.4 GHz nominal clock, profiles/ubench/) is spent on nothing but the mads of
-    # a product — no carries, loads or control: `peak` for the kernel's 9 x 29-bit product (162
-    # mads), `peak_8x32` for the 128 mads of 8 x 32-bit limbs (the fewest 32x32-bit partial products
-    # a 254-bit Montgomery product can have on this ISA). Timed with HIP events on the MSM's stream
-    # around the k_accumulate launch alone.
-    acc_ms = ph[1]
-    mults = 10 * entries.value
-    achieved = mults / (acc_ms / 1e3) / 1e9
-    peak = MAD_PEAK / MADS_PER_PRODUCT_29 / 1e9
-    peak32 = MAD_PEAK / MADS_PER_PRODUCT_32 / 1e9
-    traffic = None
-    pmc_path = os.path.join(HERE, "profiles", "pmc_accumulate.json")
-    if os.path.exists(pmc_path):
-        try:
-            with open(pmc_path) as fh:
-                traffic = json.load(fh).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    roofline = {"bound": "valu", "kernel": "k_accumulate", "achieved": round(achieved, 2), "peak": round(peak, 2),
-                "unit": "G Fq-products/s", "frac": round(achieved / peak, 4),
-                "peak_8x32": round(peak32, 2), "frac_8x32": round(achieved / peak32, 4), "traffic": traffic,
-                "peak_note": f"v_mad_u64_u32 issue rate ({MAD_CYCLES} SIMD cycles per wave64 instruction, 256 CUs x 4 "
-                             f"SIMDs, 2.4 GHz) / mads per product: 162 (9 x 29-bit, peak) or 128 (8 x 32-bit, peak_8x32)",
-                "bound_note": "integer-VALU issue bound (254-bit Montgomery products on v_mad_u64_u32): neither the "
-                              "HBM roof (the kernel moves ~1 TB/s of 8) nor MFMA (no dense contraction) applies",
-                "mad_issue_frac": round(entries.value * MADS_PER_ADD / (acc_ms / 1e3) / MAD_PEAK, 4),
-                "g1_adds_per_s": round(entries.value / (acc_ms / 1e3)),
-                "algorithmic_bytes_per_launch": 68 * entries.value,
-                "hbm_gbps_algorithmic": round(68 * entries.value / (acc_ms / 1e3) / 1e9, 1)}
-
-    # ---------------- proof-level HBM view (north star: achieved HBM-bandwidth fraction). Bytes per
-    # proof = SURVEY.md §8d's count over the REFERENCE op list, B_gs(n) = 131 E = 4192 n (grand-sum,
-    # k = 1, no selectors); the re-planned GPU path moves fewer, so this is an upper-bound view.
-    b_proof = (4192 if args.kind == "grandsum" else 101 * 32) * n
-    hbm_view = {"algorithmic_bytes_per_proof": b_proof, "achieved_GBps": round(b_proof * value / 1e9, 1),
-                "peak_GBps": 8000.0, "frac": round(b_proof * value / 1e9 / 8000.0, 4),
-                "accumulate_pmc_GBps": round(traffic / (acc_ms / 1e3) / 1e9, 1) if traffic else None,
-                "note": "the proof is INT-VALU bound (MSM bucket accumulation), not HBM bound"}
-
-    # ---------------- CPU baseline (oracle/c port of the reference op list), N = 1 only
-    log("CPU baseline")
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        try:
-            sys.path.insert(0, HERE)
-            from oracle import cbackend
-            cpu = cbackend.cpu_baseline(nbits, args.kind, threads=args.cpu_threads, ptau=ptau)
-        except Exception as e:  # baseline failure must not hide the GPU number
-            cpu = {"error": str(e)[:200]}
-
-    out = {
-        "metric": "grand-sum proofs/sec + MSM G1-adds/sec at n=2^20, 1/2/4/8 MI355X",
-        "value": round(value, 4),
-        "unit": "proofs/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u32 limbs (BN254 Fr/Fq Montgomery: 8 x 32-bit; MSM buckets 9 x 29-bit), int VALU",
-        "data": "synthetic (PCG64-seeded multisets, T = rot(F); synthetic ptau, tau = keccak('kgs-bench-tau'))",
-        "config": {"workload": f"{args.kind} prover, n=2^{nbits}, k={args.npols}, no selectors, inputs resident in HBM",
-                   "nbits": nbits, "npols": args.npols, "selectors": False, "parallelism": f"replicas x{world}", "inflight_per_gpu": args.inflight,
-                   "srs_power": power, "srs_points_resident": npts, "srs_gen_s": round(t_gen, 2),
-                   "srs_load_s": round(t_load, 2)},
-        "proof_verified": proof_verified,
-        "host_buffer_boundary": host_leg,
-        "latency_ms_single_proof": round(latency_ms, 3),
-        "round_ms_single_proof": [round(x, 3) for x in rounds],
-        "msm": msm,
-        "roofline": roofline,
-        "hbm_view": hbm_view,
-        "extra_configs": extra_cfg,
-        "cpu_baseline": cpu,
-    }
-    print(json.dumps(out))
+    if wd is not None:
+        wd.cancel()
+    emit()
     if dist:
         dist.barrier()
         dist.destroy_process_group()
