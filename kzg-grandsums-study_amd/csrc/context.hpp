@@ -293,12 +293,18 @@ void coset_inv(kgs_ctx& c, uint32_t* out, const uint32_t* in, int lcs);
 
 // MSM commitment: device Pippenger -> c bit-sum points T_k (this rank's partial, pinned host)
 struct Commit {
-  uint8_t* h_T = nullptr;  // pinned, c x 128 B (this rank's partial)
+  uint8_t* h_T = nullptr;   // pinned, c x 128 B (this rank's partial)
   uint64_t N = 0;
+  uint8_t* h_T2 = nullptr;  // second point range's partial (commit_launch_split), or nullptr
 };
 void shard_range(uint64_t n, int rank, int world, uint64_t& lo, uint64_t& hi);
 void fork_lanes(kgs_ctx& c);
 Commit commit_launch(kgs_ctx& c, const uint32_t* scalars, uint64_t N, int slot, int lane = 0);
+// latency mode (two MSM lanes, one unsharded context): points [0, cut) on lane 0 and [cut, N) on
+// lane 1 (slots slot, slot + 1); the two partials are summed by commits_finish. Otherwise the same
+// as commit_launch on `lane`.
+Commit commit_launch_split(kgs_ctx& c, const uint32_t* scalars, uint64_t N, uint64_t cut, int slot);
+bool split_commits(const kgs_ctx& c);
 // MSM over `count` scalars whose SRS points are pbase + pstride * i (a rank's slice of a
 // distributed polynomial); N = the polynomial's global point count (0: infinity)
 Commit commit_launch_slice(kgs_ctx& c, const uint32_t* scalars, uint64_t count, uint64_t pbase, uint64_t pstride,

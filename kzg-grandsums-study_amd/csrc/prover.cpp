@@ -329,6 +329,16 @@ Commit commit_launch(kgs_ctx& c, const uint32_t* scalars, uint64_t N, int slot, 
   return cm;
 }
 
+bool split_commits(const kgs_ctx& c) { return c.msm_lanes >= 2 && c.shard_world == 1; }
+
+Commit commit_launch_split(kgs_ctx& c, const uint32_t* scalars, uint64_t N, uint64_t cut, int slot) {
+  if (!split_commits(c) || cut == 0 || cut >= N) return commit_launch(c, scalars, N, slot, 0);
+  Commit a = commit_launch_slice(c, scalars, cut, 0, 1, N, slot, 0);
+  Commit b = commit_launch_slice(c, scalars + (size_t)8 * cut, N - cut, cut, 1, N, slot + 1, 1);
+  a.h_T2 = b.h_T;
+  return a;
+}
+
 // sum_k 2^k sum_r T_k^(r) -> affine LEM
 void combine_partials(const uint8_t* T_all, size_t part_stride, int nparts, int cc, uint8_t out[64]) {
   host::G1 acc = host::G1::inf();
@@ -348,9 +358,18 @@ void commits_finish_with(kgs_ctx& c, const std::vector<Commit>& cms, std::vector
   bool any = false;
   for (auto& cm : cms) any |= cm.N > 0;
   if (world == 1 || !any) {
+    std::vector<uint8_t> two;
     for (size_t i = 0; i < cms.size(); i++) {
-      if (cms[i].N) combine_partials(cms[i].h_T, tb, 1, cc, outs[i]);
-      else host::G1::inf().to_affine_lem(outs[i]);
+      if (cms[i].N && cms[i].h_T2) {  // split over the two lanes: both partials
+        two.resize(2 * tb);
+        memcpy(two.data(), cms[i].h_T, tb);
+        memcpy(two.data() + tb, cms[i].h_T2, tb);
+        combine_partials(two.data(), tb, 2, cc, outs[i]);
+      } else if (cms[i].N) {
+        combine_partials(cms[i].h_T, tb, 1, cc, outs[i]);
+      } else {
+        host::G1::inf().to_affine_lem(outs[i]);
+      }
     }
     return;
   }
@@ -717,7 +736,11 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   launch_quotient(c.st, !gs, sel, Qc, cosS, cosF, cosT, cosSF, cosST, nxm1, d_qs, lcs, rot);
   coset_inv(c, Qc, Qc, lcs);
   check_launch();
-  Commit cQ = commit_launch(c, Qc, qlen, slot++);
+  // latency mode: Q's 2n points over both MSM lanes (one lane's sort and tail overlap the other's
+  // accumulation)
+  fork_lanes(c);
+  Commit cQ = commit_launch_split(c, Qc, qlen, qlen / 2, slot);
+  slot += 2;
   HC(hipMemcpyAsync(h_flags, flags, 64, hipMemcpyDeviceToHost, c.st));
   c.sync();
   if (h_flags[1]) throw KgsError(KGS_E_NOT_DIVISIBLE, "Polynomial is not divisible");
@@ -822,8 +845,11 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
                 c.buf("div_carry2", 32 * (ntiles + 1)));
   check_launch();
   fork_lanes(c);
-  Commit cW1 = commit_launch(c, Wx, L - 1, slot++, 0);
+  // two lanes: W_xw (n - 1 points) and W_x (L - 1) balanced as W_x[0, h) on lane 0 and W_xw +
+  // W_x[h, L - 1) on lane 1, h = half of all their points
   Commit cW2 = commit_launch(c, Wxw, n - 1, slot++, 1);
+  Commit cW1 = commit_launch_split(c, Wx, L - 1, (L - 1 + n - 1) / 2, slot);
+  slot += 2;
   HC(hipMemcpyAsync(h_flags, flags, 64, hipMemcpyDeviceToHost, c.st));
   c.sync();
   if (h_flags[2] || h_flags[3]) throw KgsError(KGS_E_DOES_NOT_DIVIDE, "Polynomial does not divide");
