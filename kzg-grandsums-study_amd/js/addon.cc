@@ -7,6 +7,7 @@
 #include <string.h>
 #include <sys/mman.h>
 #include <map>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -140,11 +141,29 @@ void out_release(uint8_t* p, size_t len) {
 }
 }  // namespace
 
+
+// External memory adopted by JS but not yet reported to V8. Reporting it (napi_adjust_external_memory)
+// can start a full GC right there; done in the completion callback, that GC ran before the proof's
+// Promise resolved (+6 ms per proof at n = 2^20). It is reported when the next proof has been
+// queued instead (flush_external), so the GC overlaps that proof's GPU work. Main thread only.
+static int64_t g_ext_pending = 0;
+static void flush_external(napi_env env) {
+  if (g_ext_pending > 0) {
+    int64_t adj = 0;
+    napi_adjust_external_memory(env, g_ext_pending, &adj);
+    g_ext_pending = 0;
+  }
+}
+
 static void out_finalize(napi_env env, void* data, void* hint) {
-  const size_t len = (size_t)(uintptr_t)hint;
-  int64_t adj = 0;
-  napi_adjust_external_memory(env, -(int64_t)len, &adj);
-  out_release((uint8_t*)data, len);
+  const int64_t len = (int64_t)(uintptr_t)hint;
+  if (g_ext_pending >= len) {
+    g_ext_pending -= len;  // not reported yet
+  } else {
+    int64_t adj = 0;
+    napi_adjust_external_memory(env, -len, &adj);
+  }
+  out_release((uint8_t*)data, (size_t)len);
 }
 
 // Uint8Array over an out_alloc'd buffer handed to JS without a copy (recycled by the GC finalizer)
@@ -154,8 +173,7 @@ static napi_value adopt_u8(napi_env env, uint8_t* data, size_t len) {
     out_release(data, len);
     return nullptr;
   }
-  int64_t adj = 0;
-  napi_adjust_external_memory(env, (int64_t)len, &adj);
+  g_ext_pending += (int64_t)len;
   napi_create_typedarray(env, napi_uint8_array, len, ab, 0, &ta);
   return ta;
 }
@@ -273,10 +291,17 @@ struct Job {
   std::vector<napi_ref> refs;
   bool selected = false;
   bool want_mont = true;  // false: no Montgomery write-back (the other ranks of a distributed proof)
+  double exec_ms = 0;     // wall time of job_execute (the libkgs call on the worker thread)
 };
 
 static void job_execute(napi_env, void* data) {
   Job* j = (Job*)data;
+  const auto t0 = std::chrono::steady_clock::now();
+  struct Stamp {
+    Job* j;
+    std::chrono::steady_clock::time_point t0;
+    ~Stamp() { j->exec_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+  } stamp{j, t0};
   if (j->op == 0) {
     j->rc = kgs_srs_load_ptau(j->ctx, j->path.c_str(), j->nbits_max);
   } else {
@@ -339,6 +364,9 @@ static void job_complete(napi_env env, napi_status, void* data) {
     napi_create_array(env, &arr);
     for (size_t i = 0; i < j->mt.size(); i++) napi_set_element(env, arr, (uint32_t)i, adopt_u8(env, j->mt[i], E));
     napi_set_named_property(env, o, "montT", arr);
+    napi_value ems;
+    napi_create_double(env, j->exec_ms, &ems);
+    napi_set_named_property(env, o, "execMs", ems);  // diagnostics: time inside libkgs
     j->mf.clear();
     j->mt.clear();
     napi_resolve_deferred(env, j->deferred, o);
@@ -359,6 +387,7 @@ static napi_value queue(napi_env env, Job* j, const char* name) {
   napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &rname);
   NAPI_CALL(env, napi_create_async_work(env, nullptr, rname, job_execute, job_complete, j, &j->work));
   NAPI_CALL(env, napi_queue_async_work(env, j->work));
+  if (j->op == 1) flush_external(env);  // a GC it starts now runs beside the proof just queued
   return promise;
 }
 
@@ -533,6 +562,25 @@ static napi_value MsmPoints(napi_env env, napi_callback_info info) {
   return make_u8(env, out, 64);
 }
 
+// lastTiming(ctx) -> [round 1..5 ms, -, input copy, prover, write-back wait] of the context's last
+// kgs_prove call (kgs_last_timing; diagnostics, call when the context is idle)
+static napi_value LastTiming(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  kgs_ctx_t* ctx = get_ctx(env, argv[0]);
+  double t[9] = {0};
+  const int n = kgs_last_timing(ctx, t, 9);
+  napi_value arr;
+  napi_create_array(env, &arr);
+  for (int i = 0; i < n; i++) {
+    napi_value v;
+    napi_create_double(env, t[i], &v);
+    napi_set_element(env, arr, (uint32_t)i, v);
+  }
+  return arr;
+}
+
 static napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor desc[] = {
       {"ctxCreate", nullptr, CtxCreate, nullptr, nullptr, nullptr, napi_default, nullptr},
@@ -547,6 +595,7 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"groupCreateLocal", nullptr, GroupCreateLocal, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"ctxSetGroup", nullptr, CtxSetGroup, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"msmPoints", nullptr, MsmPoints, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"lastTiming", nullptr, LastTiming, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(desc) / sizeof(desc[0]), desc);
   return exports;
