@@ -392,8 +392,9 @@ def main():
         phase = (ctypes.c_double * 4)()
         entries = ctypes.c_uint64()
         reps = args.msm_reps
-        K._check(K.lib().kgs_bench_msm_phases(ctx.handle, ctypes.c_void_p(sc.data_ptr()), n, reps, phase,
-                                              ctypes.byref(entries)))
+        with roctx_range("kgs_bench_msm_leg"):  # lets a rocprofv3 trace be cut to these dispatches
+            K._check(K.lib().kgs_bench_msm_phases(ctx.handle, ctypes.c_void_p(sc.data_ptr()), n, reps, phase,
+                                                  ctypes.byref(entries)))
         ph = [phase[i] / reps for i in range(4)]
         msm_ms = sum(ph)
         W = (255 + window_c - 1) // window_c
