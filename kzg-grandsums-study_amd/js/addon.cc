@@ -515,6 +515,22 @@ static napi_value CtxSetGroup(napi_env env, napi_callback_info info) {
   return nullptr;
 }
 
+// ctxSetMsmLanes(ctx, lanes): 2 = the single-proof latency mode, 1 = throughput (several proofs in
+// flight on the device) — kgs_ctx_set_msm_lanes; call while the context is idle
+static napi_value CtxSetMsmLanes(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  kgs_ctx_t* ctx = get_ctx(env, argv[0]);
+  int32_t lanes = 2;
+  napi_get_value_int32(env, argv[1], &lanes);
+  if (kgs_ctx_set_msm_lanes(ctx, lanes) != KGS_OK) {
+    napi_throw_error(env, nullptr, kgs_last_error());
+    return nullptr;
+  }
+  return nullptr;
+}
+
 // pairingEq(g1s, g2s): g1s = n x 64 B affine LEM G1, g2s = n x 128 B affine LEM G2 -> bool
 // (curve.pairingEq, src/grandsum/mset_eq_kzg_verifier.js:182)
 static napi_value PairingEq(napi_env env, napi_callback_info info) {
@@ -596,6 +612,7 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"ctxSetGroup", nullptr, CtxSetGroup, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"msmPoints", nullptr, MsmPoints, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"lastTiming", nullptr, LastTiming, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"ctxSetMsmLanes", nullptr, CtxSetMsmLanes, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(desc) / sizeof(desc[0]), desc);
   return exports;

@@ -8,8 +8,8 @@
 // serialises calls per context with a mutex, and shares the read-only SRS / NTT tables between the
 // contexts of a device, so a pool of several contexts costs one set of tables per GPU.
 //
-// Knobs: KGS_JS_CONTEXTS = contexts per device (default 4: the proofs in flight that keep one
-// MI355X busy), KGS_DEVICES = comma-separated device list (default: every visible device),
+// Knobs: KGS_JS_CONTEXTS = contexts per device (default 8: with 16 concurrent calls, 8 contexts
+// reach 82 proofs/s at n = 2^20 against 78.5 with 4, profiles/r02/js_adaptive_lanes.txt), KGS_DEVICES = comma-separated device list (default: every visible device),
 // KGS_JS_SHARD_RANKS / KGS_JS_SHARD_MIN_NBITS = one large proof over several GPUs (below).
 const path = require("path");
 
@@ -35,8 +35,8 @@ function devices() {
 }
 
 function perDevice() {
-    const v = parseInt(process.env.KGS_JS_CONTEXTS || "4", 10);
-    return Number.isFinite(v) && v >= 1 ? v : 4;
+    const v = parseInt(process.env.KGS_JS_CONTEXTS || "8", 10);
+    return Number.isFinite(v) && v >= 1 ? v : 8;
 }
 
 const pool = { slots: [], idle: [], waiters: [], devs: null, cap: 0 };
@@ -48,7 +48,7 @@ function newSlot() {
     }
     // round-robin over devices: slot i lives on device devs[i % ndev]
     const device = pool.devs[pool.slots.length % pool.devs.length];
-    const slot = { device, ctx: load().ctxCreate(device), index: pool.slots.length };
+    const slot = { device, ctx: load().ctxCreate(device), index: pool.slots.length, busy: false, lanes: 2 };
     pool.slots.push(slot);
     return slot;
 }
@@ -68,10 +68,25 @@ function release(slot) {
 // run fn(slot) with exclusive use of one context
 async function withContext(fn) {
     const slot = await acquire();
+    slot.busy = true;
     try {
         return await fn(slot);
     } finally {
+        slot.busy = false;
         release(slot);
+    }
+}
+
+// MSM lanes of a proof about to start: two (single-proof latency mode, kgs_ctx_set_msm_lanes) when it
+// is alone on its device, one when other proofs are in flight there or waiting for a context — the
+// GPU is then already full, and the two-lane accumulation's register reservation would keep the
+// other contexts' kernels from co-residing (DESIGN.md §3 register budget)
+function setLanes(slot) {
+    const others = pool.slots.some(s => s !== slot && s.busy && s.device === slot.device);
+    const lanes = others || pool.waiters.length > 0 ? 1 : 2;
+    if (slot.lanes !== lanes) {
+        load().ctxSetMsmLanes(slot.ctx, lanes);
+        slot.lanes = lanes;
     }
 }
 
@@ -87,6 +102,7 @@ async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT) {
     if (shardRanks() >= 2 && nBits >= shardMinBits()) return proveSharded(kind, key, nBits, evalsF, evalsT, selF, selT);
     return withContext(async slot => {
         await load().srsLoadPtau(slot.ctx, key, nBits);
+        setLanes(slot);
         return load().prove(slot.ctx, kind, nBits, evalsF, evalsT, selF, selT);
     });
 }
