@@ -155,6 +155,7 @@ struct kgs_ctx {
   hipStream_t st2 = nullptr;
   hipStream_t st_copy = nullptr;  // Montgomery write-back of the host-buffer boundary
   hipEvent_t ev_fork = nullptr, ev_copy = nullptr;
+  std::vector<hipEvent_t> ev_in;  // kgs_prove: one per input vector DMA'd on the copy stream
   MsmWork mw2;
   int msm_lanes = 2;  // kgs_ctx_set_msm_lanes
   uint64_t msm_nseg_max = 0;
@@ -184,6 +185,7 @@ struct kgs_ctx {
     if (h_io) hipHostFree(h_io);
     if (ev_fork) hipEventDestroy(ev_fork);
     if (ev_copy) hipEventDestroy(ev_copy);
+    for (hipEvent_t e : ev_in) hipEventDestroy(e);
     if (st_copy) hipStreamDestroy(st_copy);
     if (st2) hipStreamDestroy(st2);
     if (st) hipStreamDestroy(st);
@@ -350,6 +352,9 @@ struct ProveIn {
   const uint32_t *sel_f = nullptr, *sel_t = nullptr;  // device, Montgomery (nullptr: unselected)
   std::vector<uint8_t*> mont_f_out, mont_t_out;  // host outputs (may be empty)
   std::function<void()> after_round1;             // called once round 1 is synchronised
+  // kgs_prove: per input vector (F_i at 2i, T_i at 2i + 1, then selF, selT) an event the main stream
+  // waits for before the vector's first kernel, or nullptr (already ordered on the main stream)
+  std::vector<hipEvent_t> ready;
 };
 enum R5Poly { R5_S, R5_Q, R5_F, R5_T, R5_SELF, R5_SELT, R5_POLT };
 struct R5Term {

@@ -591,12 +591,17 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
 
   // ---------------- round 1: witness polynomials + commitments (prover.js:144-179)
   std::vector<uint32_t*> fm(k), tm(k), Fc(k), Tc(k);
+  auto wait_input = [&](size_t v) {  // pipelined host-buffer inputs (kgs_prove)
+    if (v < in.ready.size() && in.ready[v]) HC(hipStreamWaitEvent(c.st, in.ready[v], 0));
+  };
   for (int i = 0; i < k; i++) {
     fm[i] = c.buf("fm" + std::to_string(i), E);
     tm[i] = c.buf("tm" + std::to_string(i), E);
     Fc[i] = c.buf("Fc" + std::to_string(i), E);
     Tc[i] = c.buf("Tc" + std::to_string(i), E);
+    wait_input(2 * i);
     launch_to_mont(c.st, fm[i], in.f_std[i], n);
+    wait_input(2 * i + 1);
     launch_to_mont(c.st, tm[i], in.t_std[i], n);
     intt_nat(c, Fc[i], fm[i], nbits);
     intt_nat(c, Tc[i], tm[i], nbits);
@@ -622,7 +627,9 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   if (sel) {
     sFc = c.buf("sFc", E);
     sTc = c.buf("sTc", E);
+    wait_input(2 * k);
     intt_nat(c, sFc, in.sel_f, nbits);
+    wait_input(2 * k + 1);
     intt_nat(c, sTc, in.sel_t, nbits);
   }
   std::vector<Commit> r1;
@@ -1145,11 +1152,39 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   using hclk = std::chrono::steady_clock;
   const auto h0 = hclk::now();
   Range rin("kgs.host.input_copy");
-  par_copy(in_jobs);
+  if (ctx->group) {  // the distributed prover reads every input at once
+    par_copy(in_jobs);
+    for (size_t v = 0; v < in_jobs.size(); v++)
+      HC(hipMemcpyAsync(dsts[v], in_jobs[v].dst, E, hipMemcpyHostToDevice, ctx->st));
+  } else {
+    // pipelined: vector v's host copy into its pinned slot overlaps vector v - 1's DMA; vector 0
+    // goes on the main stream, the others on the copy stream with an event that the main stream
+    // waits for right before the vector's first kernel, so F_0's transform starts while the rest
+    // are still in flight. (The Montgomery write-back later reuses the same pinned slots on the
+    // copy stream, after these DMAs in stream order.)
+    if (!ctx->st_copy) {
+      HC(hipStreamCreateWithFlags(&ctx->st_copy, hipStreamNonBlocking));
+      HC(hipEventCreateWithFlags(&ctx->ev_copy, hipEventDisableTiming));
+    }
+    while (ctx->ev_in.size() < in_jobs.size()) {
+      hipEvent_t e;
+      HC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ctx->ev_in.push_back(e);
+    }
+    in.ready.assign(in_jobs.size(), nullptr);
+    for (size_t v = 0; v < in_jobs.size(); v++) {
+      par_copy({in_jobs[v]});
+      if (v == 0) {
+        HC(hipMemcpyAsync(dsts[v], in_jobs[v].dst, E, hipMemcpyHostToDevice, ctx->st));
+      } else {
+        HC(hipMemcpyAsync(dsts[v], in_jobs[v].dst, E, hipMemcpyHostToDevice, ctx->st_copy));
+        HC(hipEventRecord(ctx->ev_in[v], ctx->st_copy));
+        in.ready[v] = ctx->ev_in[v];
+      }
+    }
+  }
   rin.pop();
   const auto h1 = hclk::now();
-  for (size_t v = 0; v < in_jobs.size(); v++)
-    HC(hipMemcpyAsync(dsts[v], in_jobs[v].dst, E, hipMemcpyHostToDevice, ctx->st));
   for (int i = 0; i < npols; i++) {
     in.f_std.push_back(dsts[2 * i]);
     in.t_std.push_back(dsts[2 * i + 1]);
