@@ -1,5 +1,5 @@
-// Shared body of the two drop-in verifiers (src/grandsum/mset_eq_kzg_verifier.js:9,
-// src/grandproduct/mset_eq_kzg_verifier.js:9): the proof's shape is read from its keys exactly as
+// Shared body of the drop-in verifiers (src/grandsum/mset_eq_kzg_verifier.js:9,
+// src/grandproduct/mset_eq_kzg_verifier.js:9, and the lookup one): the proof's shape is read from its keys exactly as
 // the reference does (nPols from /^F\d/, selectors from /^selF/), the values are laid out in the
 // C-ABI order and checked by libkgs's native verifier (transcript replay + optimal-ate pairing).
 const backend = require("./backend");

@@ -2,9 +2,12 @@
 // twin) driven through the drop-in modules, without mocha: random inputs via curve.Fr.random, T = F
 // rotated by one, selectors ones except selF[n-1] = selT[0] = 0. Like the reference's tests, every
 // proof must pass the verifier (here the drop-in verifier module: native transcript replay + pairing).
+// Plus the "standard lookup" of test/lookup_kzg_grandsum.test.js:24-44 (commented out in the
+// reference) through the lookup modules: it verifies there, and the grand-sum prover refuses it.
 const path = require("path");
 const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_grandproduct_prover,
-    mset_eq_kzg_grandsum_verifier, mset_eq_kzg_grandproduct_verifier } = require("../index");
+    mset_eq_kzg_grandsum_verifier, mset_eq_kzg_grandproduct_verifier, lookup_kzg_grandsum_prover,
+    lookup_kzg_grandsum_verifier } = require("../index");
 
 async function main() {
     const ptau = process.argv[2] || path.join("tmp", "powersOfTau28_hez_final_11.ptau");
@@ -40,6 +43,32 @@ async function main() {
             if (isValid !== true) throw new Error(`${name} nPols=${nPols} sel=${sel} nBits=${nBits}: proof rejected`);
             pass++;
         }
+    }
+    {
+        // test/lookup_kzg_grandsum.test.js:25-43: F = T with F[1] = F[n-1] = F[0]; multiplicities ones
+        // except m[0] = 3, m[1] = m[n-1] = 0
+        const nBits = 2;
+        const evalsT = Evaluations.getRandomEvals(2 ** nBits, curve);
+        const evalsF = Evaluations.fromEvals(evalsT);
+        evalsF.setEvaluation(1, evalsF.getEvaluation(0));
+        evalsF.setEvaluation(evalsF.length() - 1, evalsF.getEvaluation(0));
+        const mul = Evaluations.getOneEvals(2 ** nBits, curve);
+        mul.setEvaluation(0, Fr.e(3));
+        mul.setEvaluation(1, Fr.zero);
+        mul.setEvaluation(mul.length() - 1, Fr.zero);
+        const copy = e => Evaluations.fromEvals(e);
+        const proof = await lookup_kzg_grandsum_prover(ptau, copy(evalsF), copy(evalsT),
+            Evaluations.getOneEvals(2 ** nBits, curve), copy(mul));
+        if ((await lookup_kzg_grandsum_verifier(ptau, proof, nBits)) !== true) throw new Error("lookup proof rejected");
+        pass++;
+        let refused = false;
+        try {
+            await mset_eq_kzg_grandsum_prover(ptau, copy(evalsF), copy(evalsT), Evaluations.getOneEvals(2 ** nBits, curve), copy(mul));
+        } catch (e) {
+            refused = e.message === "Polynomial is not divisible";
+        }
+        if (!refused) throw new Error("the grand-sum prover accepted multiplicities");
+        pass++;
     }
     console.log(`reference-style cases passed: ${pass}`);
 }

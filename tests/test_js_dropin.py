@@ -107,7 +107,7 @@ def test_js_concurrent_provers_match_oracle(tmp_path):
 def test_reference_style_cases():
     out = subprocess.check_output([NODE, os.path.join(JS, "test", "reference_style.test.js"), common.oracle_ptau(9)],
                                   timeout=600)
-    assert b"reference-style cases passed: 8" in out
+    assert b"reference-style cases passed: 10" in out
 
 
 def _node_json(script):
