@@ -79,6 +79,31 @@ def make_lookup_inputs(seed, nbits, npols, unselected=0):
     return Fs, [std_bytes(t) for t in T], mont_bytes(sel), mont_bytes(m)
 
 
+def lookup_dup_table(seed, nbits):
+    """A table with every value twice (T[2j] = T[2j+1]); F rows drawn from it; each looked-up
+    value's multiplicity split at random between its two table rows."""
+    rnd = random.Random(seed)
+    n = 1 << nbits
+    vals = [rnd.randrange(R) for _ in range(n // 2)]
+    t = [vals[j // 2] for j in range(n)]
+    f = [vals[rnd.randrange(n // 2)] for _ in range(n)]
+    m = [0] * n
+    for v in f:
+        j = vals.index(v)
+        m[2 * j + rnd.randrange(2)] += 1
+    return [std_bytes(f)], [std_bytes(t)], mont_bytes([1] * n), mont_bytes(m)
+
+
+def lookup_all_zero(seed, nbits):
+    """selF and the multiplicities all zero, F unrelated to T: trivially satisfied (the reference's
+    prover warns "The selection buffers are all zeros", prover.js:66-68, and proves)."""
+    rnd = random.Random(seed)
+    n = 1 << nbits
+    f = [rnd.randrange(R) for _ in range(n)]
+    t = [rnd.randrange(R) for _ in range(n)]
+    return [std_bytes(f)], [std_bytes(t)], mont_bytes([0] * n), mont_bytes([0] * n)
+
+
 def reference_standard_lookup(seed=3, nbits=2):
     """The reference's commented-out "standard lookup" case (test/lookup_kzg_grandsum.test.js:24-44):
     T random, F = T with F[1] = F[n-1] = F[0], selF all ones, multiplicities one except m[0] = 3,

@@ -41,9 +41,19 @@ for npols, unselected in ((1, 0), (1, 1), (3, 0), (2, 1)):
         seed += 1
 
 
+LOOKUP_CASES += [dict(kind="lookup", gen="dup_table", nbits=3, npols=1, unselected=0, seed=2100),
+                 dict(kind="lookup", gen="dup_table", nbits=5, npols=1, unselected=0, seed=2101),
+                 dict(kind="lookup", gen="all_zero", nbits=3, npols=1, unselected=8, seed=2102),
+                 dict(kind="lookup", gen="random_table", nbits=3, npols=12, unselected=2, seed=2103)]
+
+
 def lookup_inputs(c):
     if c["gen"] == "reference_standard":
         return common.reference_standard_lookup(c["seed"], c["nbits"])
+    if c["gen"] == "dup_table":
+        return common.lookup_dup_table(c["seed"], c["nbits"])
+    if c["gen"] == "all_zero":
+        return common.lookup_all_zero(c["seed"], c["nbits"])
     return common.make_lookup_inputs(c["seed"], c["nbits"], c["npols"], c["unselected"])
 
 

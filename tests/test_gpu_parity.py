@@ -206,6 +206,25 @@ def test_trivial_identity_multiset(K):
         assert got == exp
 
 
+def test_all_zero_selectors(K):
+    """selF = selT = 0 with F, T unrelated: trivially satisfied — the reference only warns "The
+    selection buffers are all zeros" (src/grandsum/mset_eq_kzg_prover.js:66-68) and proves; S = 0 and
+    Z = 1, so several commitments are of constant polynomials. Byte-exact vs the oracle, verified."""
+    ptau = common.oracle_ptau(9)
+    srs = P.SRS(ptau, common.tau())
+    Fs, _, _, _ = common.make_inputs(31, 4, 2, False)
+    Ts, _, _, _ = common.make_inputs(32, 4, 2, False)
+    zero = common.mont_bytes([0] * 16)
+    for kind, fn, vf in (("grandsum", K.grandsum_prover, K.grandsum_verifier),
+                         ("grandproduct", K.grandproduct_prover, K.grandproduct_verifier)):
+        got = fn(ptau, [K.Evaluations(x) for x in Fs], [K.Evaluations(x) for x in Ts],
+                 K.Evaluations(zero), K.Evaluations(zero))
+        exp = P.prove(kind, srs, [P.EvalBuffer(x) for x in Fs], [P.EvalBuffer(x) for x in Ts],
+                      P.EvalBuffer(zero), P.EvalBuffer(zero))
+        assert got == exp
+        assert vf(ptau, got, 4) is True
+
+
 def _bary_eval(vals, nbits, x):
     """p(x) from evaluations on <w_n> (barycentric), O(n) with one batch inversion."""
     n = 1 << nbits

@@ -32,6 +32,10 @@ def case_id(c):
 def case_inputs(c):
     if c["gen"] == "reference_standard":
         return common.reference_standard_lookup(c["seed"], c["nbits"])
+    if c["gen"] == "dup_table":
+        return common.lookup_dup_table(c["seed"], c["nbits"])
+    if c["gen"] == "all_zero":
+        return common.lookup_all_zero(c["seed"], c["nbits"])
     return common.make_lookup_inputs(c["seed"], c["nbits"], c["npols"], c["unselected"])
 
 
