@@ -28,8 +28,12 @@ Extra fields in the JSON line:
   extra_configs : BASELINE.json configs[2] (grand-product at n), configs[3] (grand-sum n = 2^24) and
               configs[4] (selected-vector k = 4, n = 2^22) — single GPU at N = 1; at N > 1 ONE proof at
               a time over all ranks with the distributed prover (every vector sharded; RCCL
-              all-to-all / all-gather; strong scaling); each checks a proof and that ranks agree
+              all-to-all / all-gather; strong scaling); each checks a proof and that ranks agree.
+              They run last, under a watchdog (--legs-timeout, default 300 s): if a leg hangs, the
+              line is printed without the rest (extra_configs.timeout says so) and every rank exits
   cpu_baseline : the CPU port of the reference op list (oracle/c, OpenMP) on the same workload
+roctx ranges "kgs_bench_timed_region" and "kgs_bench_msm_leg" let a rocprofv3 --marker-trace run be cut
+to the headline's proofs and to the MSM leg (profiles/summarize_window.py).
 """
 import argparse
 import ctypes
