@@ -26,6 +26,7 @@
 #include <stdexcept>
 #include <string>
 #include <functional>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -1086,14 +1087,22 @@ int kgs_ptau_write_synthetic(kgs_ctx_t* ctx, const char* path, int power, const 
 }  // extern "C"
 
 namespace kgsi {
-// host copies between pageable caller buffers and the pinned staging area, split over threads
+// host copies between pageable caller buffers and the pinned staging area, split over threads; the
+// 16 threads (a GPU's host share) are divided among the contexts copying at the same time, so that
+// several proofs in flight through the host-buffer boundary do not oversubscribe the cores
+static std::atomic<int> g_copy_active{0};
 void par_copy(const std::vector<CopyJob>& jobs) {
   const size_t piece = 1u << 20;
   std::vector<CopyJob> pieces;
   for (const auto& j : jobs)
     for (size_t o = 0; o < j.len; o += piece) pieces.push_back({j.dst + o, j.src + o, std::min(piece, j.len - o)});
+  struct Active {
+    int n;
+    Active() : n(g_copy_active.fetch_add(1) + 1) {}
+    ~Active() { g_copy_active.fetch_sub(1); }
+  } active;
   unsigned nth = std::thread::hardware_concurrency();
-  nth = std::max(1u, std::min(nth, 16u));
+  nth = std::max(1u, std::min(nth, 16u) / (unsigned)std::max(1, active.n));
   if (pieces.size() < 2 || nth == 1) {
     for (const auto& p : pieces) memcpy(p.dst, p.src, p.len);
     return;
