@@ -193,6 +193,10 @@ int kgs_last_timing(kgs_ctx_t* ctx, double* rounds_ms, int max_rounds);
 /* ---- primitives (host buffers in/out; used by tests and by the bench's roofline legs) ---- */
 /* [ffjs] Fr.batchToMontgomery */
 int kgs_fr_to_mont(kgs_ctx_t* ctx, const uint8_t* in_std, uint8_t* out_mont, uint64_t n);
+/* [ffjs] Fr.batchFromMontgomery (polynomial.js:1112): out = in * 2^-256, canonical */
+int kgs_fr_from_mont(kgs_ctx_t* ctx, const uint8_t* in_mont, uint8_t* out_std, uint64_t n);
+/* [ffjs] Fr.batchInverse (grandsum.js:41, grandproduct.js:36): out[i] = in[i]^-1, zero stays zero */
+int kgs_fr_batch_inverse(kgs_ctx_t* ctx, const uint8_t* in_mont, uint8_t* out_mont, uint64_t n);
 /* [ffjs] Fr.fft / Fr.ifft: natural order in and out, size 2^logm, ifft includes 1/m */
 int kgs_ntt(kgs_ctx_t* ctx, const uint8_t* in_mont, uint8_t* out_mont, int logm, int inverse);
 /* [ffjs] G1.multiExpAffine(SRS[0..n), fromMont(scalars)) + toAffine (polynomial.js:1106-1115) */

@@ -69,6 +69,8 @@ def lib():
                                       ctypes.POINTER(ctypes.c_int)]
         L.kgs_last_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.kgs_fr_to_mont.argtypes = [ctypes.c_void_p, c_u8p, c_u8p, ctypes.c_uint64]
+        L.kgs_fr_from_mont.argtypes = [ctypes.c_void_p, c_u8p, c_u8p, ctypes.c_uint64]
+        L.kgs_fr_batch_inverse.argtypes = [ctypes.c_void_p, c_u8p, c_u8p, ctypes.c_uint64]
         L.kgs_ntt.argtypes = [ctypes.c_void_p, c_u8p, c_u8p, ctypes.c_int, ctypes.c_int]
         L.kgs_msm.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint64, c_u8p]
         L.kgs_grand_build.argtypes = [ctypes.c_void_p, ctypes.c_int, c_u8p, c_u8p, c_u8p, c_u8p, c_u8p,
@@ -377,6 +379,18 @@ class Context:
         n = len(data) // 32
         out = ctypes.create_string_buffer(32 * n)
         _check(lib().kgs_fr_to_mont(self._h, _buf(data), out, n))
+        return out.raw
+
+    def fr_from_mont(self, data):
+        n = len(data) // 32
+        out = ctypes.create_string_buffer(32 * n)
+        _check(lib().kgs_fr_from_mont(self._h, _buf(data), out, n))
+        return out.raw
+
+    def fr_batch_inverse(self, data):
+        n = len(data) // 32
+        out = ctypes.create_string_buffer(32 * n)
+        _check(lib().kgs_fr_batch_inverse(self._h, _buf(data), out, n))
         return out.raw
 
     def ntt(self, data, inverse=False):

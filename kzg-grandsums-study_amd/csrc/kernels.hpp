@@ -80,6 +80,7 @@ void launch_eval_tiles(hipStream_t st, uint32_t* part, const EvalBatch& eb, cons
 void launch_divide(hipStream_t st, uint32_t* q, uint32_t* flag, const uint32_t* a, uint64_t L, const uint32_t* xp,
                    uint32_t* part, uint32_t* carry);
 void launch_fr_batch_inv(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t n);
+void launch_from_mont(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t n);
 void launch_nxm1(hipStream_t st, uint32_t* out, const uint32_t* tw, uint64_t halfM, const uint32_t* gp,
                  const uint32_t* np, int lcs, uint64_t wstride);
 constexpr uint64_t EVAL_TILE = 2048;

@@ -30,6 +30,16 @@ __global__ void k_to_mont(uint32_t* __restrict__ out, const uint32_t* __restrict
 void launch_to_mont(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t n) {
   hipLaunchKernelGGL(k_to_mont, dim3(nb(n)), dim3(256), 0, st, out, in, n);
 }
+// [ffjs] Fr.batchFromMontgomery (polynomial.js:1112, before G1.multiExpAffine)
+__global__ void k_from_mont(uint32_t* __restrict__ out, const uint32_t* __restrict__ in, uint64_t n) {
+  KGS_AUX_PRIO();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fr::load(in + 8 * i).from_mont().store(out + 8 * i);
+}
+void launch_from_mont(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t n) {
+  hipLaunchKernelGGL(k_from_mont, dim3(nb(n)), dim3(256), 0, st, out, in, n);
+}
 
 // ---------------------------------------------------------------------------- linear combination
 __global__ void k_lincomb(uint32_t* __restrict__ out, uint64_t n, LinComb lc) {

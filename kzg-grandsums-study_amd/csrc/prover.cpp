@@ -1279,6 +1279,34 @@ int kgs_fr_to_mont(kgs_ctx_t* ctx, const uint8_t* in_std, uint8_t* out_mont, uin
   API_END
 }
 
+// the shim's elementwise maps (host buffers in and out, one launch on ctx's stream)
+static void fr_map(kgs_ctx_t* ctx, const uint8_t* in, uint8_t* out, uint64_t n,
+                   void (*launch)(hipStream_t, uint32_t*, const uint32_t*, uint64_t)) {
+  if (!ctx || (n && (!in || !out))) throw KgsError(KGS_E_ARG, "NULL argument");
+  if (!n) return;
+  CTX_LOCK(ctx);
+  HC(hipSetDevice(ctx->device));
+  uint32_t* a = ctx->buf("prim_a", 32 * n);
+  uint32_t* b = ctx->buf("prim_b", 32 * n);
+  HC(hipMemcpyAsync(a, in, 32 * n, hipMemcpyHostToDevice, ctx->st));
+  launch(ctx->st, b, a, n);
+  check_launch();
+  HC(hipMemcpyAsync(out, b, 32 * n, hipMemcpyDeviceToHost, ctx->st));
+  ctx->sync();
+}
+
+int kgs_fr_from_mont(kgs_ctx_t* ctx, const uint8_t* in_mont, uint8_t* out_std, uint64_t n) {
+  API_BEGIN
+  fr_map(ctx, in_mont, out_std, n, launch_from_mont);
+  API_END
+}
+
+int kgs_fr_batch_inverse(kgs_ctx_t* ctx, const uint8_t* in_mont, uint8_t* out_mont, uint64_t n) {
+  API_BEGIN
+  fr_map(ctx, in_mont, out_mont, n, launch_fr_batch_inv);
+  API_END
+}
+
 int kgs_ntt(kgs_ctx_t* ctx, const uint8_t* in_mont, uint8_t* out_mont, int logm, int inverse) {
   API_BEGIN
   if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");

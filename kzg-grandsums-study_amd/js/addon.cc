@@ -276,7 +276,7 @@ struct Job {
   napi_async_work work = nullptr;
   napi_deferred deferred = nullptr;
   kgs_ctx_t* ctx = nullptr;
-  int op = 0;  // 0 = load ptau, 1 = prove
+  int op = 0;  // 0 = load ptau, 1 = prove, 2 = elementwise Fr map / transform (frOp)
   int rc = 0;
   std::string err;
   // load
@@ -292,6 +292,11 @@ struct Job {
   bool selected = false;
   bool want_mont = true;  // false: no Montgomery write-back (the other ranks of a distributed proof)
   double exec_ms = 0;     // wall time of job_execute (the libkgs call on the worker thread)
+  // frOp
+  int fr_op = 0;
+  View in;
+  uint8_t* out = nullptr;  // out_alloc'd, adopted by JS on success
+  size_t out_len = 0;
 };
 
 static void job_execute(napi_env, void* data) {
@@ -304,6 +309,23 @@ static void job_execute(napi_env, void* data) {
   } stamp{j, t0};
   if (j->op == 0) {
     j->rc = kgs_srs_load_ptau(j->ctx, j->path.c_str(), j->nbits_max);
+  } else if (j->op == 2) {
+    const uint64_t n = j->in.len / 32;
+    j->out_len = j->in.len;
+    j->out = out_alloc(j->out_len);
+    if (!j->out) {
+      j->rc = KGS_E_ARG;
+      j->err = "out of host memory";
+      return;
+    }
+    int logm = 0;
+    while ((1ull << logm) < n) logm++;
+    switch (j->fr_op) {
+      case 0: j->rc = kgs_fr_to_mont(j->ctx, j->in.p, j->out, n); break;
+      case 1: j->rc = kgs_fr_from_mont(j->ctx, j->in.p, j->out, n); break;
+      case 2: j->rc = kgs_fr_batch_inverse(j->ctx, j->in.p, j->out, n); break;
+      default: j->rc = kgs_ntt(j->ctx, j->in.p, j->out, logm, j->fr_op == 4); break;
+    }
   } else {
     int nc = 0, ne = 0;
     kgs_proof_shape(j->kind, j->npols, j->selected ? 1 : 0, &nc, &ne);
@@ -348,6 +370,9 @@ static void job_complete(napi_env env, napi_status, void* data) {
     napi_value u;
     napi_get_undefined(env, &u);
     napi_resolve_deferred(env, j->deferred, u);
+  } else if (j->op == 2) {
+    napi_resolve_deferred(env, j->deferred, adopt_u8(env, j->out, j->out_len));
+    j->out = nullptr;
   } else {
     napi_value o, arr;
     napi_create_object(env, &o);
@@ -376,6 +401,7 @@ static void job_complete(napi_env env, napi_status, void* data) {
     if (p) out_release(p, Eo);
   for (uint8_t* p : j->mt)
     if (p) out_release(p, Eo);
+  if (j->out) out_release(j->out, j->out_len);
   for (napi_ref r : j->refs) napi_delete_reference(env, r);
   napi_delete_async_work(env, j->work);
   delete j;
@@ -442,6 +468,33 @@ static napi_value Prove(napi_env env, napi_callback_info info) {
     if (ty == napi_boolean) napi_get_value_bool(env, argv[7], &j->want_mont);
   }
   return queue(env, j, "kgs_prove");
+}
+
+// frOp(ctx, op, Uint8Array) -> Promise<Uint8Array> on ctx's GPU, elementwise over 32 B elements:
+// op 0 = Fr.batchToMontgomery, 1 = Fr.batchFromMontgomery, 2 = Fr.batchInverse (0 -> 0),
+// 3 = Fr.fft, 4 = Fr.ifft (2^k elements, natural order) — the curve shim's batch members
+static napi_value FrOp(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Job* j = new Job();
+  j->op = 2;
+  j->ctx = get_ctx(env, argv[0]);
+  napi_get_value_int32(env, argv[1], &j->fr_op);
+  j->in = view_of(env, argv[2], j->refs);
+  const uint64_t n = j->in.len / 32;
+  const bool pow2 = n && !(n & (n - 1));
+  const char* bad = j->fr_op < 0 || j->fr_op > 4                  ? "frOp: unknown op"
+                    : !n || j->in.len % 32                        ? "frOp: the buffer must hold 32-byte elements"
+                    : j->fr_op >= 3 && (!pow2 || n > (1ull << 28)) ? "frOp: fft size must be a power of two <= 2^28"
+                                                                   : nullptr;
+  if (bad) {
+    for (napi_ref r : j->refs) napi_delete_reference(env, r);
+    delete j;
+    napi_throw_error(env, nullptr, bad);
+    return nullptr;
+  }
+  return queue(env, j, "kgs_fr_op");
 }
 
 // verifyPtau(kind, ptauPath, nbits, npols, selected, commitments(Uint8Array), evaluations(Uint8Array))
@@ -613,6 +666,7 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"msmPoints", nullptr, MsmPoints, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"lastTiming", nullptr, LastTiming, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"ctxSetMsmLanes", nullptr, CtxSetMsmLanes, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"frOp", nullptr, FrOp, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(desc) / sizeof(desc[0]), desc);
   return exports;

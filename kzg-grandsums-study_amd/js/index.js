@@ -1,6 +1,8 @@
 // JavaScript host of the MI355X prover: the reference's module surface.
 module.exports = {
     getCurveFromName: require("./src/curve").getCurveFromName,
+    BigBuffer: require("./src/bigbuffer").BigBuffer,
+    Scalar: require("./src/scalar").Scalar,
     Evaluations: require("./src/polynomial/evaluations").Evaluations,
     mset_eq_kzg_grandsum_prover: require("./src/grandsum/mset_eq_kzg_prover"),
     mset_eq_kzg_grandproduct_prover: require("./src/grandproduct/mset_eq_kzg_prover"),

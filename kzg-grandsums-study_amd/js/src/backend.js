@@ -12,6 +12,7 @@
 // reach 82 proofs/s at n = 2^20 against 78.5 with 4, profiles/r02/js_adaptive_lanes.txt), KGS_DEVICES = comma-separated device list (default: every visible device),
 // KGS_JS_SHARD_RANKS / KGS_JS_SHARD_MIN_NBITS = one large proof over several GPUs (below).
 const path = require("path");
+const { contiguous } = require("./bigbuffer");
 
 // N-API async work runs on the libuv thread pool (4 threads by default): one thread per context of
 // an 8-GPU pool needs more. Effective only if set before the process first uses the pool.
@@ -99,6 +100,12 @@ function ptauPower(pTauFilename) {
 // and prove on the same held context: nothing can swap the SRS between the two
 async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT) {
     const key = path.resolve(pTauFilename);
+    // evaluations held in a BigBuffer (Evaluations.fromPolynomial, src/polynomial/evaluations.js:12-21)
+    // go to the native side as one contiguous copy
+    evalsF = evalsF.map(contiguous);
+    evalsT = evalsT.map(contiguous);
+    if (selF) selF = contiguous(selF);
+    if (selT) selT = contiguous(selT);
     if (shardRanks() >= 2 && nBits >= shardMinBits()) return proveSharded(kind, key, nBits, evalsF, evalsT, selF, selT);
     return withContext(async slot => {
         await load().srsLoadPtau(slot.ctx, key, nBits);

@@ -2,6 +2,9 @@
 // (SURVEY.md §8b), in ffjavascript's in-memory formats:
 //   Fr, F1 {n8, p, zero, one, negone, two, w[], e, add, sub, mul, neg, square, inv, div, eq, isZero,
 //           random, toString, toRprBE, toRprLE, toObject, fromMontgomery, toMontgomery}
+//   Fr     {fft, ifft, batchInverse, batchToMontgomery, batchFromMontgomery}: on the GPU through the
+//           addon (kgs_ntt / kgs_fr_batch_inverse / kgs_fr_to_mont / kgs_fr_from_mont), Promises of
+//           the input's buffer kind (Uint8Array, or BigBuffer for a BigBuffer)
 //   G1 {F, zero, one, zeroAffine, oneAffine, add, sub, neg, double, eq, isZero, timesFr,
 //       timesScalar, toAffine, toJacobian, isValid, toRprUncompressed, fromRprUncompressed,
 //       toRprLEM, fromRprLEM, toObject, fromObject, toString, multiExpAffine}
@@ -13,6 +16,7 @@
 // and curve.pairingEq through the native optimal-ate pairing (kgs_pairing_eq). The hot path itself
 // is libkgs's prover.
 const crypto = require("crypto");
+const { BigBuffer, contiguous } = require("./bigbuffer");
 
 const R = 21888242871839275222246405745257275088548364400416034343698204186575808495617n;
 const Q = 21888242871839275222246405745257275088696311157297823662689037894645226208583n;
@@ -273,6 +277,28 @@ function buildBn128() {
     let w = modpow(5n, (R - 1n) >> 28n, R);
     for (let k = 28; k >= 0; k--) { Fr.w[k] = Fr.e(w); w = (w * w) % R; }
     const addon = () => require("./backend.js").load();
+    // [ffjs] Fr batch members (grandsum.js:41 batchInverse, polynomial.js:34,152,160 fft / ifft,
+    // polynomial.js:1112 batchFromMontgomery, prover.js:147-148 batchToMontgomery)
+    async function frOp(op, buff) {
+        const flat = contiguous(buff);
+        if (flat.byteLength % 32) throw new Error("Fr: the buffer must hold 32-byte elements");
+        let out;
+        if (flat.byteLength === 0) {
+            out = new Uint8Array(0);
+        } else {
+            const a = addon();
+            out = await a.frOp(shimContext(a), op, flat);
+        }
+        if (!(buff instanceof BigBuffer)) return out;
+        const bb = new BigBuffer(out.byteLength);
+        bb.set(out, 0);
+        return bb;
+    }
+    Fr.batchToMontgomery = (buff) => frOp(0, buff);
+    Fr.batchFromMontgomery = (buff) => frOp(1, buff);
+    Fr.batchInverse = (buff) => frOp(2, buff);  // zero elements stay zero
+    Fr.fft = (buff) => frOp(3, buff);           // 2^k elements, natural order, w = Fr.w[k]
+    Fr.ifft = (buff) => frOp(4, buff);          // includes the 1/2^k
     const G1 = buildG1(F1, Fr, addon);
     const G2 = buildG2(F1);
     return {

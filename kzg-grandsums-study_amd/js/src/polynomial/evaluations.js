@@ -1,8 +1,10 @@
 // Evaluation-form vector: the prover's input container. Same surface as the reference's
 // src/polynomial/evaluations.js:5-136 (fromArray, fromEvals, getOneEvals, getZeroEvals,
 // getRandomEvals, getRandomBinEvals, getEvaluation, getEvaluationSequence, setEvaluation, length,
-// isEqual, isAllZeros, isAllOnes). `fromPolynomial` (the fft helper) is not needed by callers: the
-// prover's NTTs run on the GPU.
+// isEqual, isAllZeros, isAllOnes), and fromPolynomial through the curve shim's GPU Fr.fft. The
+// prover itself does not use fromPolynomial: its NTTs run inside libkgs.
+const { BigBuffer } = require("../bigbuffer");
+
 class Evaluations {
     constructor(evaluations, curve) {
         this.eval = evaluations;
@@ -13,6 +15,15 @@ class Evaluations {
         const buffer = new Uint8Array(array.length * curve.Fr.n8);
         for (let i = 0; i < array.length; i++) buffer.set(array[i], i * curve.Fr.n8);
         return new Evaluations(buffer, curve);
+    }
+    // evaluations.js:12-21: zero-pad the coefficients (by buffer length, not degree) to
+    // 2^ceil(log2 len) * extension and take the forward DFT
+    static async fromPolynomial(polynomial, extension, curve) {
+        const power = Math.ceil(Math.log2(polynomial.length()));
+        const length = (1 << power) * extension;
+        const coefficientsN = new BigBuffer(length * curve.Fr.n8);
+        coefficientsN.set(polynomial.coef, 0);
+        return new Evaluations(await curve.Fr.fft(coefficientsN), curve);
     }
     static fromEvals(evals) { return new Evaluations(evals.eval.slice(), evals.curve); }
     static getOneEvals(length, curve) {

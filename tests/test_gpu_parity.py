@@ -57,6 +57,22 @@ def test_to_mont(ctx9):
     assert ctx9.fr_to_mont(common.std_bytes(v)) == common.mont_bytes(v)
 
 
+def test_from_mont_and_batch_inverse(ctx9):
+    # [ffjs] Fr.batchFromMontgomery / Fr.batchInverse (grandsum.js:41): ragged sizes across the
+    # 32-element per-thread chunks, zeros (kept zero), one and r - 1
+    rnd = random.Random(3)
+    for n in (1, 2, 31, 32, 33, 777, 4099):
+        v = rv(rnd, n)
+        v[0] = 0
+        if n > 2:
+            v[1], v[-1] = 1, R - 1
+        if n > 40:
+            v[32] = v[33] = 0
+        assert ctx9.fr_from_mont(common.mont_bytes(v)) == common.std_bytes(v)
+        assert unmb(ctx9.fr_batch_inverse(common.mont_bytes(v))) == [pow(x, R - 2, R) for x in v]
+    assert ctx9.fr_from_mont(b"") == b"" and ctx9.fr_batch_inverse(b"") == b""
+
+
 # 0..10: radix-8/4/2 passes only; 11..17: LDS-staged passes of 6/5/4 stages (k_ntt_lds_pass<3,3>,
 # <3,2>, <2,2>) followed by radix-8/4/2 passes, in every combination (11 = 6+5, 13 = 6+6+1,
 # 14 = 6+6+2, 15 = 6+6+3, 16 = 6+6+4, 17 = 6+6+5)

@@ -192,6 +192,113 @@ getCurveFromName('bn128').then(async c => {{
     assert bytes.fromhex(_node_json(script)["r"]) == want
 
 
+def test_bigbuffer_and_scalar():
+    """[ffjs] BigBuffer (paged bytes: set / slice across a page boundary, flattening) and Scalar
+    (fromRprLE / fromRprBE / lt: Keccak256Transcript.js:50, mset_eq_kzg_verifier.js:195). Host only.
+    The multi-page paths run on a small BigBuffer whose 2^30-byte pages are replaced by short
+    arrays."""
+    script = """
+const { BigBuffer, Scalar } = require('./index.js');
+const { contiguous } = require('./src/bigbuffer.js');
+const out = {};
+const bb = new BigBuffer(100);
+out.pages = bb.buffers.length;
+bb.set(Uint8Array.from([1, 2, 3]), 97);
+out.tail = Array.from(bb.slice(96, 100));
+out.neg = Array.from(bb.slice(-3));
+// two short pages standing in for 2^30-byte ones
+const big = new BigBuffer(0);
+big.byteLength = 6; big.buffers = [Uint8Array.from([9, 8, 7]), Uint8Array.from([6, 5, 4])];
+out.flat = Array.from(contiguous(big));
+const dst = new BigBuffer(8);
+dst.set(big, 1);
+out.set_bb = Array.from(dst.slice(0, 8));
+const le = Uint8Array.from([1, 2, 0, 0]);
+out.le = Scalar.fromRprLE(le, 0, 4).toString();
+out.be = Scalar.fromRprBE(le, 0, 4).toString();
+out.le_off = Scalar.fromRprLE(le, 1, 1).toString();
+out.lt = [Scalar.lt(1n, 2n), Scalar.lt(2n, 2n), Scalar.lt(Scalar.fromRprLE(new Uint8Array(32).fill(255)),
+          21888242871839275222246405745257275088548364400416034343698204186575808495617n)];
+const rp = new Uint8Array(4); Scalar.toRprBE(rp, 0, 0x01020304n, 4);
+out.rprbe = Array.from(rp);
+process.stdout.write(JSON.stringify(out));
+"""
+    o = _node_json(script)
+    assert o["pages"] == 1
+    assert o["tail"] == [0, 1, 2, 3] and o["neg"] == [1, 2, 3]
+    assert o["flat"] == [9, 8, 7, 6, 5, 4]
+    assert o["set_bb"] == [0, 9, 8, 7, 6, 5, 4, 0]
+    assert o["le"] == str(0x0201) and o["be"] == str(0x01020000) and o["le_off"] == "2"
+    assert o["lt"] == [True, False, False]
+    assert o["rprbe"] == [1, 2, 3, 4]
+
+
+@pytest.mark.gpu
+def test_curve_shim_fr_batch_members_on_gpu(tmp_path):
+    """Fr.fft / ifft / batchInverse / batchToMontgomery / batchFromMontgomery of the shim
+    (grandsum.js:41, polynomial.js:34,152,160,1112, prover.js:147-148) run on the GPU through the
+    addon and match the oracle, for Uint8Array and BigBuffer inputs; Evaluations.fromPolynomial
+    (evaluations.js:12-21) pads and transforms; a prover input held in a BigBuffer proves the same
+    as the Uint8Array one."""
+    import random
+    from oracle import bn254 as bn
+    from oracle import poly as OP
+    rnd = random.Random(11)
+    R = bn.R
+    v = [rnd.randrange(R) for _ in range(64)]
+    v[5] = 0
+    (tmp_path / "v.bin").write_bytes(common.mont_bytes(v))
+    (tmp_path / "s.bin").write_bytes(common.std_bytes(v))
+    coef = v[:20]
+    Fs, Ts, _, _ = common.make_inputs(77, 4, 1, False)
+    (tmp_path / "f.bin").write_bytes(Fs[0])
+    (tmp_path / "t.bin").write_bytes(Ts[0])
+    ptau = common.oracle_ptau(9)
+    script = f"""
+const fs = require('fs');
+const {{ getCurveFromName, BigBuffer, Evaluations, mset_eq_kzg_grandsum_prover: prover }} = require('./index.js');
+const hex = (b) => Buffer.from(b instanceof BigBuffer ? b.slice(0, b.byteLength) : b).toString('hex');
+getCurveFromName('bn128').then(async c => {{
+  const v = new Uint8Array(fs.readFileSync('{tmp_path / "v.bin"}'));
+  const s = new Uint8Array(fs.readFileSync('{tmp_path / "s.bin"}'));
+  const bb = new BigBuffer(v.byteLength); bb.set(v, 0);
+  const o = {{}};
+  o.fft = hex(await c.Fr.fft(v));
+  o.ifft = hex(await c.Fr.ifft(v));
+  const fb = await c.Fr.fft(bb);
+  o.fft_bb_kind = fb instanceof BigBuffer;
+  o.fft_bb = hex(fb);
+  o.fft1 = hex(await c.Fr.fft(v.slice(0, 32)));
+  o.inv = hex(await c.Fr.batchInverse(v));
+  o.tomont = hex(await c.Fr.batchToMontgomery(s));
+  o.frommont = hex(await c.Fr.batchFromMontgomery(v));
+  o.empty = (await c.Fr.batchInverse(new Uint8Array(0))).byteLength;
+  try {{ await c.Fr.fft(v.slice(0, 96)); o.bad = 'no error'; }} catch (e) {{ o.bad = e.message; }}
+  const poly = {{ coef: v.slice(0, {32 * len(coef)}), length() {{ return this.coef.byteLength / 32; }} }};
+  o.frompoly = hex((await Evaluations.fromPolynomial(poly, 2, c)).eval);
+  const f = new Uint8Array(fs.readFileSync('{tmp_path / "f.bin"}')), t = new Uint8Array(fs.readFileSync('{tmp_path / "t.bin"}'));
+  const p1 = await prover('{ptau}', new Evaluations(f.slice(), c), new Evaluations(t.slice(), c));
+  const fB = new BigBuffer(f.byteLength); fB.set(f, 0);
+  const tB = new BigBuffer(t.byteLength); tB.set(t, 0);
+  const p2 = await prover('{ptau}', new Evaluations(fB, c), new Evaluations(tB, c));
+  o.bb_proof_same = JSON.stringify(p1, (k, x) => x instanceof Uint8Array ? hex(x) : x) ===
+                    JSON.stringify(p2, (k, x) => x instanceof Uint8Array ? hex(x) : x);
+  process.stdout.write(JSON.stringify(o));
+}});
+"""
+    o = _node_json(script)
+    mb = lambda xs: common.mont_bytes(xs).hex()
+    assert o["fft"] == mb(OP.ntt(v, False)) and o["ifft"] == mb(OP.ntt(v, True))
+    assert o["fft_bb_kind"] is True and o["fft_bb"] == o["fft"]
+    assert o["fft1"] == mb(v[:1])
+    assert o["inv"] == mb([pow(x, R - 2, R) for x in v])
+    assert o["tomont"] == mb(v) and o["frommont"] == common.std_bytes(v).hex()
+    assert o["empty"] == 0
+    assert "power of two" in o["bad"]
+    assert o["frompoly"] == mb(OP.ntt(coef + [0] * 44, False))  # 20 -> 2^5 * 2 = 64
+    assert o["bb_proof_same"] is True
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("ranks", [2, 4])
 def test_js_sharded_prover_matches_oracle(tmp_path, ranks):
