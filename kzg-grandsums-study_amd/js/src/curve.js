@@ -280,6 +280,12 @@ function buildBn128() {
     // [ffjs] Fr batch members (grandsum.js:41 batchInverse, polynomial.js:34,152,160 fft / ifft,
     // polynomial.js:1112 batchFromMontgomery, prover.js:147-148 batchToMontgomery)
     async function frOp(op, buff) {
+        if (Array.isArray(buff)) {  // an array of elements in, an array of elements out
+            const packed = new Uint8Array(32 * buff.length);
+            buff.forEach((e, i) => packed.set(e, 32 * i));
+            const out = await frOp(op, packed);
+            return buff.map((_, i) => out.slice(32 * i, 32 * i + 32));
+        }
         const flat = contiguous(buff);
         if (flat.byteLength % 32) throw new Error("Fr: the buffer must hold 32-byte elements");
         let out;

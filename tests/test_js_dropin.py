@@ -273,6 +273,11 @@ getCurveFromName('bn128').then(async c => {{
   o.tomont = hex(await c.Fr.batchToMontgomery(s));
   o.frommont = hex(await c.Fr.batchFromMontgomery(v));
   o.empty = (await c.Fr.batchInverse(new Uint8Array(0))).byteLength;
+  const arr = await c.Fr.batchInverse([v.slice(0, 32), v.slice(32, 64), v.slice(160, 192)]);
+  o.arr = arr.map(hex);
+  const big = new Uint8Array(32 << 16);
+  for (let i = 0; i < 1 << 16; i++) big.set(c.Fr.e(BigInt(i) * 7919n + 3n), 32 * i);
+  o.roundtrip = hex(await c.Fr.ifft(await c.Fr.fft(big))) === hex(big);
   try {{ await c.Fr.fft(v.slice(0, 96)); o.bad = 'no error'; }} catch (e) {{ o.bad = e.message; }}
   const poly = {{ coef: v.slice(0, {32 * len(coef)}), length() {{ return this.coef.byteLength / 32; }} }};
   o.frompoly = hex((await Evaluations.fromPolynomial(poly, 2, c)).eval);
@@ -294,6 +299,8 @@ getCurveFromName('bn128').then(async c => {{
     assert o["inv"] == mb([pow(x, R - 2, R) for x in v])
     assert o["tomont"] == mb(v) and o["frommont"] == common.std_bytes(v).hex()
     assert o["empty"] == 0
+    assert o["arr"] == [common.mont_bytes([pow(x, R - 2, R)]).hex() for x in (v[0], v[1], v[5])]
+    assert o["roundtrip"] is True
     assert "power of two" in o["bad"]
     assert o["frompoly"] == mb(OP.ntt(coef + [0] * 44, False))  # 20 -> 2^5 * 2 = 64
     assert o["bb_proof_same"] is True
