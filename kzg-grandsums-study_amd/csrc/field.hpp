@@ -221,6 +221,17 @@ struct Fe {
     for (int i = 0; i < 8; i++) d.v[i] = borrow ? e.v[i] : d.v[i];
     return d;
   }
+  // a - b + 2p in (0, 4p) for a, b in [0, 2p), no conditional correction: a multiplicand of
+  // mul_nored (whose product is still < 2p when the other factor is < p: 4p * p / 2^256 < 0.76 p)
+  __device__ __forceinline__ static Fe sub_2p(const Fe& a, const Fe& b) {
+    Fe s;
+    uint32_t c = 0, borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = __builtin_addc(a.v[i], p2(i), c, &c);
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = __builtin_subc(s.v[i], b.v[i], borrow, &borrow);
+    return s;
+  }
   __device__ __forceinline__ bool is_zero_lazy() const {  // == 0 mod p for a value in [0, 2p)
     uint32_t z = 0, q = 0;
 #pragma unroll

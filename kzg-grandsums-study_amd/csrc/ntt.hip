@@ -9,6 +9,11 @@
 // convolution path; a natural-order input to the inverse is gathered through bit reversal inside
 // the first pass. Coset scaling / 1/m scaling are fused into the first / last pass.
 //
+// Arithmetic: butterflies run on values in [0, 2p) (lazy reduction, fr::add_lazy / sub_lazy /
+// sub_2p / mul_nored): one conditional correction per sum or difference and none after a product;
+// every pass stores canonical values, so the output is bit-identical to a canonical-arithmetic
+// network. -DKGS_NTT_CANON builds the canonical butterflies (A/B).
+//
 // Twiddles: per direction one resident STAGE table tw[h + t] = w_{2h}^t (t < h, h = 1..M/2; M
 // entries for the largest domain M), so the butterflies of one stage read consecutive twiddles
 // (coalesced: consecutive lanes have consecutive t) instead of a strided walk through w_M^j.
@@ -19,6 +24,40 @@ namespace kgs {
 __device__ __forceinline__ uint32_t bitrev(uint32_t x, int bits) {
   return __builtin_bitreverse32(x) >> (32 - bits);
 }
+
+#ifndef KGS_NTT_CANON
+// DIF butterfly (a, b) -> (a + b, (a - b) w), t == 0: w = 1; inputs and outputs in [0, 2p)
+__device__ __forceinline__ void bfly_dif(fr& x0, fr& x1, const uint32_t* w, bool tw) {
+  const fr a = x0, b = x1;
+  x0 = fr::add_lazy(a, b);
+  x1 = tw ? fr::mul_nored(fr::sub_2p(a, b), fr::load(w)) : fr::sub_lazy(a, b);
+}
+// DIT butterfly (a, b) -> (a + b w, a - b w); inputs and outputs in [0, 2p)
+__device__ __forceinline__ void bfly_dit(fr& x0, fr& x1, const uint32_t* w, bool tw) {
+  const fr a = x0;
+  const fr b = tw ? fr::mul_nored(x1, fr::load(w)) : x1;
+  x0 = fr::add_lazy(a, b);
+  x1 = fr::sub_lazy(a, b);
+}
+__device__ __forceinline__ fr canon_out(const fr& x) { return x.canon(); }
+#else
+__device__ __forceinline__ void bfly_dif(fr& x0, fr& x1, const uint32_t* w, bool tw) {
+  const fr a = x0, b = x1;
+  x0 = a + b;
+  fr diff = a - b;
+  if (tw) diff = diff * fr::load(w);
+  x1 = diff;
+}
+__device__ __forceinline__ void bfly_dit(fr& x0, fr& x1, const uint32_t* w, bool tw) {
+  const fr a = x0;
+  fr b = x1;
+  if (tw) b = b * fr::load(w);
+  x0 = a + b;
+  x1 = a - b;
+}
+__device__ __forceinline__ fr canon_out(const fr& x) { return x; }
+#endif
+
 
 // One pass of K DIF stages starting at global stage s0 (stage s has half-distance m >> (s+1)).
 // If `in` != nullptr this is the first pass: read in[idx] (zero beyond in_len), optionally
@@ -64,15 +103,11 @@ __global__ void __launch_bounds__(256) k_ntt_dif_pass(uint32_t* __restrict__ dat
       // j-th butterfly of this stage: register pair (r, r + dist), r has bit (K-1-k) clear
       const int r = ((j / dist) * 2 * dist) + (j % dist);
       const uint64_t t = lo + ((uint64_t)(j % dist) << logd);
-      fr a = x[r], b = x[r + dist];
-      x[r] = a + b;
-      fr diff = a - b;
-      if (t) diff = diff * fr::load(tw + 8 * (twbase + t));
-      x[r + dist] = diff;
+      bfly_dif(x[r], x[r + dist], tw + 8 * (twbase + t), t != 0);
     }
   }
 #pragma unroll
-  for (int r = 0; r < (1 << K); r++) x[r].store(data + 8 * (base + ((uint64_t)r << logd)));
+  for (int r = 0; r < (1 << K); r++) canon_out(x[r]).store(data + 8 * (base + ((uint64_t)r << logd)));
 }
 
 // One pass of K DIT stages starting at global stage s0 (half-distance 2^s). First pass may read
@@ -113,10 +148,7 @@ __global__ void __launch_bounds__(256) k_ntt_dit_pass(uint32_t* __restrict__ dat
     for (int j = 0; j < (1 << (K - 1)); j++) {
       const int r = ((j / dist) * 2 * dist) + (j % dist);
       const uint64_t t = lo + ((uint64_t)(j % dist) << logd);
-      fr a = x[r], b = x[r + dist];
-      if (t) b = b * fr::load(tw + 8 * (twbase + t));
-      x[r] = a + b;
-      x[r + dist] = a - b;
+      bfly_dit(x[r], x[r + dist], tw + 8 * (twbase + t), t != 0);
     }
   }
   fr ps;
@@ -127,7 +159,7 @@ __global__ void __launch_bounds__(256) k_ntt_dit_pass(uint32_t* __restrict__ dat
     fr y = x[r];
     if (post) y = y * fr::load(post + 8 * idx);
     if (post_s) y = y * ps;
-    y.store(data + 8 * idx);
+    canon_out(y).store(data + 8 * idx);
   }
 }
 
@@ -180,17 +212,10 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
       const uint64_t idx = lds_idx(col, jb + js * r, K, logd);
       const uint64_t t = idx & ((1ull << logh) - 1);
       const uint32_t* w = tw + 8 * ((1ull << logh) + t);  // stage table: w_{2h}^t = tw[h + t]
-      fr a = x[r], b = x[r + dist];
-      if (DIT) {
-        if (t) b = b * fr::load(w);
-        x[r] = a + b;
-        x[r + dist] = a - b;
-      } else {
-        x[r] = a + b;
-        fr diff = a - b;
-        if (t) diff = diff * fr::load(w);
-        x[r + dist] = diff;
-      }
+      if (DIT)
+        bfly_dit(x[r], x[r + dist], w, t != 0);
+      else
+        bfly_dif(x[r], x[r + dist], w, t != 0);
     }
   }
 #pragma unroll
@@ -260,7 +285,7 @@ __global__ void __launch_bounds__(256) k_ntt_lds_pass(uint32_t* __restrict__ dat
     fr y = fr::load(lds + 8 * (j * LB + cl));
     if (post) y = y * fr::load(post + 8 * idx);
     if (post_s) y = y * ps;
-    y.store(data + 8 * idx);
+    canon_out(y).store(data + 8 * idx);
   }
 }
 
