@@ -438,6 +438,16 @@ def main():
                     traffic = json.load(fh).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        # the clock the chip holds under this kernel and its achieved SIMD cycles per VALU instruction,
+        # from a committed counter pass (profiles/clock_accumulate.json; GRBM_GUI_ACTIVE / 8 / duration)
+        clock = None
+        clk_path = os.path.join(HERE, "profiles", "clock_accumulate.json")
+        if os.path.exists(clk_path):
+            try:
+                with open(clk_path) as fh:
+                    clock = json.load(fh)
+            except Exception:
+                clock = None
         roofline = {"bound": "valu", "kernel": "k_accumulate", "achieved": round(achieved, 2), "peak": round(peak, 2),
                     "unit": "G Fq-products/s", "frac": round(achieved / peak, 4),
                     "peak_8x32": round(peak32, 2), "frac_8x32": round(achieved / peak32, 4), "traffic": traffic,
@@ -449,6 +459,16 @@ def main():
                     "g1_adds_per_s": round(entries.value / (acc_ms / 1e3)),
                     "algorithmic_bytes_per_launch": 68 * entries.value,
                     "hbm_gbps_algorithmic": round(68 * entries.value / (acc_ms / 1e3) / 1e9, 1)}
+        if clock and clock.get("held_clock_ghz"):
+            ghz = float(clock["held_clock_ghz"])
+            roofline["held_clock"] = {
+                "ghz": ghz, "peak_at_held_clock": round(peak * ghz / 2.4, 2),
+                "frac_at_held_clock": round(achieved / (peak * ghz / 2.4), 4),
+                "simd_cycles_per_valu_instruction": clock.get("simd_cycles_per_valu_instruction"),
+                "note": "counter pass of the MSM alone (profiles/clock_accumulate.json): the chip holds ~2.07 GHz under "
+                        "this kernel, not 2.4, and it issues one VALU instruction per ~4.73 SIMD cycles against "
+                        "4.2-4.93 per instruction measured for its instruction classes (ubench_r02.txt): issue bound; "
+                        "the rest of `peak` is the carries and reductions around the mads (DESIGN.md §3)"}
 
         # ---------------- proof-level HBM view (north star: achieved HBM-bandwidth fraction). Bytes per
         # proof = SURVEY.md §8d's count over the REFERENCE op list, B_gs(n) = 131 E = 4192 n (grand-sum,
