@@ -255,6 +255,11 @@ def main():
     ap.add_argument("--inflight", type=int, default=4,
                     help="independent proofs in flight per GPU (one context + HIP stream + host thread each)")
     args = ap.parse_args()
+    # stdout carries the JSON line only: chatter that libraries write straight to fd 1 (gloo's
+    # connection report, RCCL warnings) is sent to stderr, and the line goes out on a saved copy of fd 1
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -528,14 +533,14 @@ def main():
     def emit():
         with emitted:
             if rank == 0 and not state["printed"]:
-                print(json.dumps(dict(out, extra_configs=dict(extra_cfg))), flush=True)
+                print(json.dumps(dict(out, extra_configs=dict(extra_cfg))), file=json_out, flush=True)
                 state["printed"] = True
 
     def legs_timeout():
         extra_cfg["timeout"] = f"extra legs exceeded {args.legs_timeout} s; line emitted without the rest"
         log(extra_cfg["timeout"])
         emit()
-        sys.stdout.flush()
+        json_out.flush()
         os._exit(0)
 
     wd = None
