@@ -470,10 +470,12 @@ def main():
                 "ghz": ghz, "peak_at_held_clock": round(peak * ghz / 2.4, 2),
                 "frac_at_held_clock": round(achieved / (peak * ghz / 2.4), 4),
                 "simd_cycles_per_valu_instruction": clock.get("simd_cycles_per_valu_instruction"),
-                "note": "counter pass of the MSM alone (profiles/clock_accumulate.json): the chip holds ~2.07 GHz under "
-                        "this kernel, not 2.4, and it issues one VALU instruction per ~4.73 SIMD cycles against "
-                        "4.2-4.93 per instruction measured for its instruction classes (ubench_r02.txt): issue bound; "
-                        "the rest of `peak` is the carries and reductions around the mads (DESIGN.md §3)"}
+                "issue_frac_vs_register_resident_add": clock.get("issue_frac_vs_register_resident_add"),
+                "note": "counter passes (profiles/clock_accumulate.json, real cycles = GRBM_GUI_ACTIVE/8): the chip holds "
+                        "~2.07 GHz under this kernel, not 2.4; it issues one VALU instruction per ~4.73 SIMD cycles, "
+                        "against 4.17 for the same add arithmetic register-resident (madd29 ubench): 88 % of its "
+                        "arithmetic's issue rate; the rest of `peak` is the carries and reductions around the mads "
+                        "(DESIGN.md §3)"}
 
         # ---------------- proof-level HBM view (north star: achieved HBM-bandwidth fraction). Bytes per
         # proof = SURVEY.md §8d's count over the REFERENCE op list, B_gs(n) = 131 E = 4192 n (grand-sum,
