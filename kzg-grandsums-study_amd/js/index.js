@@ -10,4 +10,6 @@ module.exports = {
     mset_eq_kzg_grandproduct_verifier: require("./src/grandproduct/mset_eq_kzg_verifier"),
     lookup_kzg_grandsum_prover: require("./src/lookup/lookup_kzg_prover"),
     lookup_kzg_grandsum_verifier: require("./src/lookup/lookup_kzg_verifier"),
+    // the provers' log channel (the reference's logger.js lines): setLogger(logplease instance), setLogLevel
+    logger: require("./src/logger"),
 };

@@ -10,6 +10,7 @@ import subprocess
 import pytest
 
 import common
+from oracle import bn254 as bn
 from oracle import protocol as P
 from oracle.keccak import keccak256
 
@@ -341,3 +342,46 @@ def test_js_sharded_prover_matches_oracle(tmp_path, ranks):
         assert "error" not in g, g
         assert {"commitments": g["commitments"], "evaluations": g["evaluations"]} == exp
         assert g["montF"] == mont
+
+
+@pytest.mark.gpu
+def test_js_prover_log_lines(tmp_path):
+    """KGS_LOG_LEVEL=INFO: a real proof through the JS module writes the reference's log lines
+    (prover.js:13-140,164-412) to stderr with the oracle's challenges; stdout is untouched; all-zero
+    selectors raise the reference's warning (prover.js:66-68) at the default level."""
+    ptau = common.oracle_ptau(9)
+    srs = P.SRS(ptau, common.tau())
+    cases, traces = [], []
+    for kind, npols, sel in (("grandsum", 2, True), ("grandproduct", 1, False)):
+        Fs, Ts, sF, sT = common.make_inputs(8100 + npols, 5, npols, sel)
+        cases.append({"kind": kind, "F": [x.hex() for x in Fs], "T": [x.hex() for x in Ts],
+                      "selF": sF.hex() if sF else None, "selT": sT.hex() if sT else None})
+        tr = {}
+        eF = [P.EvalBuffer(x) for x in Fs]
+        eT = [P.EvalBuffer(x) for x in Ts]
+        P.prove(kind, srs, eF if npols > 1 else eF[0], eT if npols > 1 else eT[0],
+                P.EvalBuffer(sF) if sF else None, P.EvalBuffer(sT) if sT else None, trace=tr)
+        traces.append(tr["challenges"])
+    spec = tmp_path / "spec.json"
+    spec.write_text(json.dumps({"ptau": ptau, "cases": cases}))
+    out = subprocess.run([NODE, os.path.join(JS, "test", "prove_from_json.js"), str(spec)], capture_output=True,
+                         text=True, timeout=600, env=dict(os.environ, KGS_LOG_LEVEL="INFO"))
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert len(json.loads(out.stdout)["proofs"]) == 2  # stdout still carries only the driver's JSON
+    log = out.stderr
+    assert log.count("PROVER STARTED") == 2 and log.count("PROVER FINISHED") == 2
+    assert "[INFO]   Domain size: 32" in log and "[INFO]   Selectors: Yes" in log
+    for ch in traces:
+        for name, sym in (("gamma", "𝜸"), ("alpha", "𝜶"), ("xi", "𝔷")):
+            assert f"···      {sym}  = {ch[name] % bn.R}" in log, name
+    # all-zero selectors: the reference's warning at the default level (the proof itself is trivial)
+    Fs, Ts, _, _ = common.make_inputs(8200, 5, 1, False)
+    zero = (b"\0" * 32 * 32).hex()
+    spec.write_text(json.dumps({"ptau": ptau, "cases": [{"kind": "grandsum", "F": [Fs[0].hex()], "T": [Ts[0].hex()],
+                                                          "selF": zero, "selT": zero}]}))
+    env = {k: v for k, v in os.environ.items() if k != "KGS_LOG_LEVEL"}
+    out = subprocess.run([NODE, os.path.join(JS, "test", "prove_from_json.js"), str(spec)], capture_output=True,
+                         text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "[WARN] The selection buffers are all zeros. The argument is trivially satisfied." in out.stderr
+    assert "[INFO]" not in out.stderr

@@ -1,0 +1,94 @@
+"""The JS drop-in provers' log lines (SURVEY.md §5 "Metrics / logging": the reference's
+logger.info / logger.warn lines, src/grandsum/mset_eq_kzg_prover.js:13-140,164-412 and the
+grand-product twin). CPU-only: the round log of every golden proof is replayed from the proof
+(js/src/prover_common.js logRounds, the transcript of src/Keccak256Transcript.js:7-53 through
+libkgs's keccak256) and its challenges must equal the oracle's recorded ones; the level switch
+(KGS_LOG_LEVEL, default WARN) and an injected logger are checked without a GPU call."""
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+import common
+from oracle import bn254 as bn
+
+JS = os.path.join(common.ROOT, "kzg-grandsums-study_amd", "js")
+ADDON = os.path.join(JS, "build", "kgs_addon.node")
+NODE = shutil.which("node")
+pytestmark = pytest.mark.skipif(NODE is None or not os.path.exists(ADDON), reason="node or the N-API addon is missing")
+
+GOLDEN = os.path.join(common.ROOT, "tests", "golden", "golden.json")
+
+
+def _replay(tmp_path):
+    g = json.load(open(GOLDEN))
+    cases = [dict(kind=c["kind"], nbits=c["nbits"], npols=c["npols"], selected=c["selected"], proof=c["proof"])
+             for c in g["cases"]]
+    spec = tmp_path / "replay.json"
+    spec.write_text(json.dumps({"cases": cases}))
+    out = subprocess.run([NODE, os.path.join(JS, "test", "replay_log.js"), str(spec)], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    return g["cases"], json.loads(out.stdout)["cases"]
+
+
+def test_replayed_challenges_match_oracle(tmp_path):
+    golden, got = _replay(tmp_path)
+    assert len(golden) == len(got) == 48
+    for c, o in zip(golden, got):
+        for k, v in c["challenges"].items():
+            assert o["challenges"][k] == v, (c["kind"], c["nbits"], c["npols"], c["selected"], k)
+
+
+def test_log_lines_follow_the_reference(tmp_path):
+    golden, got = _replay(tmp_path)
+    r = bn.R
+    for c, o in zip(golden, got):
+        lines = o["lines"]
+        gs = c["kind"] != "grandproduct"
+        vec = c["npols"] > 1
+        # prover.js:111: the plain-quoted "${round}" is printed literally by the reference
+        assert lines[0].startswith("> ROUND ${round}. Generate the witness polynomials")
+        assert ("for i ∈ [%d]" % c["npols"] in lines[0]) == vec
+        assert ("selector polynomials" in lines[0]) == c["selected"]
+        title = "GRAND-SUM" if gs else "GRAND-PRODUCT"
+        assert f"> MULTISET EQUALITY KZG {title}" in lines[-1] and lines[-1].endswith("PROVER FINISHED")
+        assert lines[-2] == ""
+        heads = [ln for ln in lines if ln.startswith("> ROUND")]
+        assert [h.split(".")[0] for h in heads] == ["> ROUND ${round}", "> ROUND 2", "> ROUND 3", "> ROUND 4", "> ROUND 5"]
+        assert (f"grand-{'sum' if gs else 'product'} polynomial {'S' if gs else 'Z'}") in heads[1]
+        # one t(z) line per multiset for the grand-sum only (grand-product prover.js:296-303)
+        tz = [ln for ln in lines if ln.startswith("···   t") and not ln.startswith("···   tsel")]
+        assert len(tz) == (c["npols"] if gs else 0)
+        assert any(ln.startswith("···      𝛃  =") for ln in lines) == vec
+        # ZH(xi) and L1(xi) (polynomial_utils.js:1-19) from the oracle's challenge
+        xi = int(c["challenges"]["xi"])
+        n = 1 << c["nbits"]
+        zh = (pow(xi, n, r) - 1) % r
+        l1 = zh * pow(n * (xi - 1) % r, r - 2, r) % r
+        assert f"···  ZH(𝔷)  = {zh}" in lines
+        assert f"···  L₁(𝔷)  = {l1}" in lines
+        # commitments as G1.toString of the affine point: "[ x, y, 1 ]"
+        q = [ln for ln in lines if ln.startswith("··· [Q(x)]₁ =")]
+        assert len(q) == 1 and q[0].endswith(", 1 ]")
+
+
+def test_log_level_switch():
+    # default WARN: info lines are dropped, warnings printed; KGS_LOG_LEVEL=INFO prints both
+    script = ("const l=require(%r); l.info('info-line'); l.warn('warn-line');" % os.path.join(JS, "src", "logger.js"))
+    env = {k: v for k, v in os.environ.items() if k != "KGS_LOG_LEVEL"}
+    # (the built-in sink writes to stderr, so a caller's stdout is untouched)
+    run = lambda e: subprocess.run([NODE, "-e", script], capture_output=True, text=True, env=e)
+    out = run(env)
+    assert out.stdout == "" and "info-line" not in out.stderr and "[WARN] warn-line" in out.stderr
+    out = run(dict(env, KGS_LOG_LEVEL="info"))
+    assert "[INFO] info-line" in out.stderr and "warn-line" in out.stderr
+    assert run(dict(env, KGS_LOG_LEVEL="NONE")).stderr == ""
+    # an injected logger (e.g. the reference's logplease instance) receives every line
+    inj = ("const l=require(%r); const got=[]; l.setLogger({info:(...a)=>got.push('I:'+a.join(' ')),"
+           "warn:(...a)=>got.push('W:'+a.join(' '))}); l.info('a', 1); l.warn('b'); console.log(JSON.stringify(got));"
+           % os.path.join(JS, "src", "logger.js"))
+    out = subprocess.run([NODE, "-e", inj], capture_output=True, text=True, env=env).stdout
+    assert json.loads(out) == ["I:a 1", "W:b"]
