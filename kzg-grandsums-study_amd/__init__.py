@@ -516,6 +516,7 @@ def _context(device=0):
 def _prover(kind, pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, device=0):
     """src/grandsum/mset_eq_kzg_prover.js:12-142 — input checks with the reference's messages, then
     the HIP prover. Overwrites evalsFs[i].eval / evalsTs[i].eval with Montgomery form (:147-148)."""
+    log.info("> MULTISET EQUALITY KZG %s PROVER STARTED", _TITLE[kind])
     power = ptau_power(pTauFilename)  # the header is read first (prover.js:15-16)
     if not isinstance(evalsFs, (list, tuple)):
         evalsFs = [evalsFs]
@@ -544,11 +545,18 @@ def _prover(kind, pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None
         raise ValueError("The selection buffers must have the same length as the multiset buffers.")
     # a lookup keeps its selectors even when all one (its proof always carries selF / selT)
     is_selected = kind == LOOKUP or not (evalsSelF.isAllOnes() and evalsSelT.isAllOnes())
+    if is_selected and evalsSelF.isAllZeros() and evalsSelT.isAllZeros():  # prover.js:66-68
+        log.warning("The selection buffers are all zeros. The argument is trivially satisfied.")
     nbits = (n0 - 1).bit_length() if n0 > 0 else 0
     if n0 != (1 << nbits):
         raise ValueError("Polynomial length must be a power of two.")
     if power < nbits:
         raise ValueError("The Powers of Tau file is not sufficiently large to commit the polynomials.")
+    if log.isEnabledFor(logging.INFO):  # prover.js:87-93
+        for line in ("-------------------------------------", f"  MULTISET EQUALITY KZG {_TITLE[kind]} PROVER SETTINGS",
+                     "  Curve:       bn128", f"  Domain size: {1 << nbits}", f"  Number of polynomials: {npols}",
+                     f"  Selectors: {'Yes' if is_selected else 'No'}", "-------------------------------------"):
+            log.info(line)
     ctx = _context(device)
     # only the 2^(nbits+1) points this proof commits with (prover.js:83-85); grow-only device cache
     ctx.load_ptau(pTauFilename, nbits)
@@ -559,7 +567,135 @@ def _prover(kind, pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None
         evalsFs[i].eval = mf[i]
         evalsTs[i].eval = mt[i]
     cn, en = proof_names(kind, npols, is_selected)
-    return {"commitments": dict(zip(cn, coms)), "evaluations": dict(zip(en, evs))}
+    proof = {"commitments": dict(zip(cn, coms)), "evaluations": dict(zip(en, evs))}
+    if log.isEnabledFor(logging.INFO):
+        log_rounds(kind, proof, nbits, npols, is_selected)
+    return proof
+
+
+# ---------------------------------------------------------------- the reference's log lines
+# logger.js (logplease at INFO) as used by src/grandsum/mset_eq_kzg_prover.js:13-140,164-412 and the
+# grand-product twin: the same messages on the standard `logging` logger "kgs" (silent until the
+# caller enables INFO on it). The proof is computed in one library call, so the round lines follow
+# it, with the challenges replayed from the proof's transcript (src/Keccak256Transcript.js:7-53).
+import logging  # noqa: E402
+
+log = logging.getLogger("kgs")
+_FQ = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+_FR = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+_TITLE = {GRANDSUM: "GRAND-SUM", GRANDPRODUCT: "GRAND-PRODUCT", LOOKUP: "GRAND-SUM (LOOKUP)"}
+
+
+def _fr_int(b):  # 32 B LE Montgomery Fr -> integer
+    return int.from_bytes(bytes(b), "little") * pow(1 << 256, _FR - 2, _FR) % _FR
+
+
+def _g1_xy(b):  # 64 B affine LEM -> (x, y) standard, None for the zero point
+    rinv = pow(1 << 256, _FQ - 2, _FQ)
+    x = int.from_bytes(bytes(b[:32]), "little") * rinv % _FQ
+    y = int.from_bytes(bytes(b[32:64]), "little") * rinv % _FQ
+    return None if x == 0 and y == 0 else (x, y)
+
+
+def _g1_str(b):  # [ffjs] G1.toString of an affine point
+    a = _g1_xy(b)
+    return "[ 0, 1, 0 ]" if a is None else f"[ {a[0]}, {a[1]}, 1 ]"
+
+
+class _Transcript:
+    """G1.toRprUncompressed (64 B big-endian x||y, the zero point 0x40 then zeros) / Fr.toRprBE (32 B);
+    a challenge is keccak256 of everything added so far, big-endian, mod r."""
+
+    def __init__(self):
+        self.buf = bytearray()
+
+    def add_commitment(self, b):
+        a = _g1_xy(b)
+        self.buf += (b"\x40" + bytes(63)) if a is None else a[0].to_bytes(32, "big") + a[1].to_bytes(32, "big")
+
+    def add_scalar(self, v):
+        self.buf += (v % _FR).to_bytes(32, "big")
+
+    def challenge(self):
+        return int.from_bytes(keccak256(bytes(self.buf)), "big") % _FR
+
+
+def log_rounds(kind, proof, nbits, npols, selected, logger=None):
+    """Write the reference's round log of `proof` (prover.js:111-140 with each round's lines) and
+    return its challenges {beta, gamma, alpha, xi, v} (beta None for k = 1)."""
+    lg = logger or log
+    gs = kind != GRANDPRODUCT
+    vec = npols > 1
+    C, E = proof["commitments"], proof["evaluations"]
+    tr = _Transcript()
+    msg = "> ROUND ${round}. Generate the witness polynomials"  # printed literally by the reference
+    msg += f" fᵢ,tᵢ ∈ 𝔽[X], for i ∈ [{npols}]" if vec else " f,t ∈ 𝔽[X]"
+    if selected:
+        msg += ", and the selector polynomials fsel,tsel ∈ 𝔽[X]"
+    lg.info(msg)
+    for i in range(npols):
+        nf, nt = (f"F{i}", f"T{i}") if vec else ("F", "T")
+        lg.info("··· [%s]₁ = %s", f"f{i + 1}(x)" if vec else "f(x)", _g1_str(C[nf]))
+        lg.info("··· [%s]₁ = %s", f"t{i + 1}(x)" if vec else "t(x)", _g1_str(C[nt]))
+        tr.add_commitment(C[nf])
+        tr.add_commitment(C[nt])
+    if selected:
+        lg.info("··· [fsel(x)]₁ = %s", _g1_str(C["selF"]))
+        lg.info("··· [tsel(x)]₁ = %s", _g1_str(C["selT"]))
+        tr.add_commitment(C["selF"])
+        tr.add_commitment(C["selT"])
+    sz = "S" if gs else "Z"
+    lg.info("> ROUND 2. Compute the grand-%s polynomial %s ∈ 𝔽[X]", "sum" if gs else "product", sz)
+    beta = None
+    if vec:
+        beta = tr.challenge()
+        lg.info("···      𝛃  = %d", beta)
+        tr.add_scalar(beta)
+    gamma = tr.challenge()
+    lg.info("···      𝜸  = %d", gamma)
+    lg.info("··· [%s(x)]₁ = %s", sz, _g1_str(C[sz]))
+    lg.info("> ROUND 3. Compute the quotient polynomial Q ∈ 𝔽[X]")
+    tr.add_scalar(gamma)
+    tr.add_commitment(C[sz])
+    alpha = tr.challenge()
+    lg.info("···      𝜶  = %d", alpha)
+    lg.info("··· [Q(x)]₁ = %s", _g1_str(C["Q"]))
+    lg.info("> ROUND 4. Compute the evaluations of the polynomials")
+    tr.add_scalar(alpha)
+    tr.add_commitment(C["Q"])
+    xi = tr.challenge()
+    lg.info("···      𝔷  = %d", xi)
+    evs = []
+    for i in range(npols):
+        fx = _fr_int(E[f"f{i}xi" if vec else "fxi"])
+        lg.info("···   %s  = %d", f"f{i + 1}(𝔷)" if vec else "f(𝔷)", fx)
+        evs.append(fx)
+        if gs:
+            tx = _fr_int(E[f"t{i}xi" if vec else "txi"])
+            lg.info("···   %s  = %d", f"t{i + 1}(𝔷)" if vec else "t(𝔷)", tx)
+            evs.append(tx)
+    if selected:
+        evs += [_fr_int(E["selFxi"]), _fr_int(E["selTxi"])]
+        lg.info("···   fsel(𝔷)  = %d", evs[-2])
+        lg.info("···   tsel(𝔷)  = %d", evs[-1])
+    zw = _fr_int(E["sxiw" if gs else "zxiw"])
+    lg.info("··· %s(𝔷·𝛚)  = %d", sz, zw)
+    lg.info("> ROUND 5. Compute the opening proof polynomials W𝔷, W𝔷𝛚 ∈ 𝔽[X]")
+    tr.add_scalar(xi)
+    for v in evs + [zw]:
+        tr.add_scalar(v)
+    v = tr.challenge()
+    lg.info("···      v  =  %d", v)
+    n = 1 << nbits
+    zh = (pow(xi, n, _FR) - 1) % _FR  # polynomial_utils.js:1-19
+    l1 = zh * pow(n * (xi - 1) % _FR, _FR - 2, _FR) % _FR
+    lg.info("···  ZH(𝔷)  = %d", zh)
+    lg.info("···  L₁(𝔷)  = %d", l1)
+    lg.info("··· [W𝔷(x)]₁   = %s", _g1_str(C["Wxi"]))
+    lg.info("··· [W𝔷·𝛚(x)]₁ = %s", _g1_str(C["Wxiw"]))
+    lg.info("")
+    lg.info("> MULTISET EQUALITY KZG %s PROVER FINISHED", _TITLE[kind])
+    return {"beta": beta, "gamma": gamma, "alpha": alpha, "xi": xi, "v": v}
 
 
 def grandsum_prover(pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, device=0):

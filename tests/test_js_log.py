@@ -92,3 +92,33 @@ def test_log_level_switch():
            % os.path.join(JS, "src", "logger.js"))
     out = subprocess.run([NODE, "-e", inj], capture_output=True, text=True, env=env).stdout
     assert json.loads(out) == ["I:a 1", "W:b"]
+
+
+def test_python_mirror_log_matches_js(tmp_path):
+    """The Python mirror (logging logger "kgs") writes the same round log as the JS modules, line for
+    line, and replays the oracle's challenges (CPU: keccak256 through libkgs, no GPU call)."""
+    import logging
+    K = common.load_pkg()
+    golden, got = _replay(tmp_path)
+    kinds = {"grandsum": K.GRANDSUM, "grandproduct": K.GRANDPRODUCT, "lookup": K.LOOKUP}
+
+    class Capture(logging.Handler):
+        def __init__(self):
+            super().__init__()
+            self.lines = []
+
+        def emit(self, record):
+            self.lines.append(record.getMessage())
+
+    lg = logging.getLogger("kgs.test")
+    lg.propagate = False
+    lg.setLevel(logging.INFO)
+    for c, o in zip(golden, got):
+        h = Capture()
+        lg.addHandler(h)
+        proof = {sec: {k: bytes.fromhex(v) for k, v in c["proof"][sec].items()} for sec in ("commitments", "evaluations")}
+        ch = K.log_rounds(kinds[c["kind"]], proof, c["nbits"], c["npols"], c["selected"], logger=lg)
+        lg.removeHandler(h)
+        assert h.lines == o["lines"], (c["kind"], c["nbits"], c["npols"], c["selected"])
+        for k, v in c["challenges"].items():
+            assert ch[k] == int(v), k
