@@ -436,6 +436,14 @@ __device__ __forceinline__ const uint32_t* run_rec(const uint32_t* raw, uint64_t
 #ifndef KGS_DIAG_GATHER_MASK
 #define KGS_DIAG_GATHER_MASK 0x7fffffffu
 #endif
+#ifdef KGS_DIAG_CLOCK
+// diagnostic builds only (-DKGS_DIAG_CLOCK; never the shipped library): thread 0 of each of the first
+// KGS_CLK_BLOCKS blocks stamps the shader clock (s_memtime) and the 100 MHz real-time counter
+// (s_memrealtime) around its add loop; the last launch's stamps give the clock the chip held while it
+// ran (kgs_diag_clock), also with other proofs' kernels in flight. Stamps go to their own buffer.
+constexpr int KGS_CLK_BLOCKS = 8192;
+__device__ unsigned long long g_kgs_clk[4 * KGS_CLK_BLOCKS];
+#endif
 template <int VW>
 __global__ void __launch_bounds__(256, VW) k_accumulate(uint32_t* __restrict__ segowner,
                                                     uint32_t* __restrict__ chunklist, uint32_t* __restrict__ chunkcnt,
@@ -448,6 +456,13 @@ __global__ void __launch_bounds__(256, VW) k_accumulate(uint32_t* __restrict__ s
   const uint64_t E = offsets[nbins];
   const uint64_t start = s * L;
   if (start >= E) return;
+#ifdef KGS_DIAG_CLOCK
+  unsigned long long clk0 = 0, rt0 = 0;
+  if (threadIdx.x == 0) {
+    clk0 = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   const uint64_t end = start + L < E ? start + L : E;
   // largest b with offsets[b] <= start (offsets nondecreasing, offsets[0] == 0)
   uint32_t lo = 0, hi = nbins;  // invariant offsets[lo] <= start < offsets[hi]
@@ -488,7 +503,36 @@ __global__ void __launch_bounds__(256, VW) k_accumulate(uint32_t* __restrict__ s
     acc.add_aff(xw, yw, negy);
   }
   acc.store_raw(run_rec(raw, rs32 == offsets[b] ? (uint64_t)b : nbins + s));
+#ifdef KGS_DIAG_CLOCK
+  if (threadIdx.x == 0 && blockIdx.x < KGS_CLK_BLOCKS) {
+    const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* o = g_kgs_clk + 4 * blockIdx.x;
+    o[0] = clk0;
+    o[1] = clk1;
+    o[2] = rt0;
+    o[3] = rt1;
+  }
+#endif
 }
+
+#ifdef KGS_DIAG_CLOCK
+// median over the stamped blocks of d(shader clock) / d(real time) x 100 MHz, in GHz
+extern "C" int kgs_diag_clock(double* ghz, int* nblocks) {
+  static unsigned long long h[4 * KGS_CLK_BLOCKS];
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_kgs_clk), sizeof(h)) != hipSuccess) return 1;
+  std::vector<double> v;
+  for (int b = 0; b < KGS_CLK_BLOCKS; b++)
+    if (h[4 * b + 3] > h[4 * b + 2] && h[4 * b + 1] > h[4 * b]) v.push_back((double)(h[4 * b + 1] - h[4 * b]) / (double)(h[4 * b + 3] - h[4 * b + 2]) * 0.1);
+  *nblocks = (int)v.size();
+  if (v.empty()) return 1;
+  std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+  *ghz = v[v.size() / 2];
+  const unsigned long long zero[4 * 64] = {};
+  for (int b = 0; b < KGS_CLK_BLOCKS; b += 64) hipMemcpyToSymbol(HIP_SYMBOL(g_kgs_clk), zero, sizeof(zero), 8 * 4 * b);
+  return 0;
+}
+#endif
 
 // Bucket totals. Bucket b = its start record (run_rec b) + the partials of the segments whose start
 // lies strictly inside it: segments s_lo(b) = offsets[b]/L + 1 .. s_hi(b) = ceil(offsets[b+1]/L) - 1.
