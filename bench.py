@@ -14,7 +14,9 @@ sync points of one proof overlap the bulk kernels of another; `latency_ms_single
 one-at-a-time latency on a single context, measured outside the timed region.
 
 N > 1 GPUs (torchrun, one process per GPU): every rank proves its own independent multisets
-(replicas, "weak" scaling); value = proofs of all ranks / max-over-ranks time.
+(replicas, "weak" scaling); value = proofs of all ranks / max-over-ranks time. `--gpus N` is the
+rank count: under a launcher WORLD_SIZE must equal it (else exit 2); started bare with N > 1 the
+script launches its own N ranks (torch.distributed.run, 127.0.0.1) as a child process.
 
 Extra fields in the JSON line:
   proof_verified : one proof of the timed workload checked with the native verifier (pairing)
@@ -31,6 +33,7 @@ Extra fields in the JSON line:
               all-to-all / all-gather; strong scaling); each checks a proof and that ranks agree.
               They run last, under a watchdog (--legs-timeout, default 300 s): if a leg hangs, the
               line is printed without the rest (extra_configs.timeout says so) and every rank exits
+              with status 3 (a hang is a failure, not a pass)
   cpu_baseline : the CPU port of the reference op list (oracle/c, OpenMP) on the same workload
 roctx ranges "kgs_bench_timed_region" and "kgs_bench_msm_leg" let a rocprofv3 --marker-trace run be cut
 to the headline's proofs and to the MSM leg (profiles/summarize_window.py).
@@ -169,10 +172,13 @@ def large_leg(K, torch, dist, rank, world, local, nb, k, selected, proofs, label
     n = 1 << nb
     log(f"large leg: {label}")
     ctx = K.Context(local)
-    t0 = time.time()
     ptau, _ = shared_ptau(ctx, nb, dist)
-    ctx.load_ptau(ptau, nb)
+    t0 = time.time()
+    # the distributed prover's ranks each hold only their SRS slice (points rank + world * j)
+    sliced = world > 1 and group is not None
+    ctx.load_ptau(ptau, nb, slice=(rank, world) if sliced else None)
     setup_s = time.time() - t0
+    table_bytes = ctx.srs_slice_info()[2]
     keep, d_f, d_t = [], [], []
     for i in range(k):
         f, t = synth_evals(n, 5000 + i)
@@ -214,7 +220,9 @@ def large_leg(K, torch, dist, rank, world, local, nb, k, selected, proofs, label
     verified = K.grandsum_verifier(ptau, {"commitments": dict(zip(cn, coms)), "evaluations": dict(zip(en, evs))}, nb)
     out = {"workload": label, "n_gpus": world, "mode": mode,
            "proofs": proofs, "ms_per_proof": round(1000.0 * el / proofs, 3),
-           "proofs_per_s": round(proofs / el, 4), "srs_setup_s": round(setup_s, 2), "proof_verified": verified,
+           "proofs_per_s": round(proofs / el, 4), "srs_setup_s_rank0": round(setup_s, 2),
+           "srs_table_bytes_rank0": table_bytes, "srs_slice": f"points r + {world} j" if sliced else "whole prefix",
+           "proof_verified": verified,
            "round_ms_last_proof_rank0": [round(x, 3) for x in ctx.last_timing()[:5]]}
     if dist:
         h = torch.tensor(list(K.keccak256(b"".join(coms))[:8]), dtype=torch.int64, device=coll_device())
@@ -227,6 +235,21 @@ def large_leg(K, torch, dist, rank, world, local, nb, k, selected, proofs, label
     del keep
     torch.cuda.empty_cache()
     return out
+
+
+def self_launch(n):
+    """Run this script as n ranks under torch.distributed.run (127.0.0.1, a free port) as a CHILD
+    process — this process has not touched a GPU — and return its exit status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"launching {n} ranks: {' '.join(cmd[2:])}")
+    return subprocess.call(cmd)
 
 
 def main():
@@ -252,9 +275,22 @@ def main():
                     help="proofs timed in the selected-vector leg (N > 1: MSMs sharded over all ranks)")
     ap.add_argument("--legs-timeout", type=float, default=300.0,
                     help="watchdog on the extra legs (seconds, 0 = none): on expiry the line is printed without them")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, join the process group, count the ranks with one collective, "
+                         "print {n_gpus, ranks_joined} from rank 0 and exit (no GPU touched; CPU test of the launch)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="independent proofs in flight per GPU (one context + HIP stream + host thread each)")
     args = ap.parse_args()
+    # --gpus N is the number of ranks. Under a launcher (torchrun / torch.distributed.run) WORLD_SIZE
+    # must agree with it; started bare with N > 1, bench.py launches its N ranks itself (one process
+    # per GPU) before anything touches a GPU and exits with the launcher's status — never a silent
+    # one-GPU run.
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}", file=sys.stderr)
+            sys.exit(2)
+    elif args.gpus > 1:
+        sys.exit(self_launch(args.gpus))
     # stdout carries the JSON line only: chatter that libraries write straight to fd 1 (gloo's
     # connection report, RCCL warnings) is sent to stderr, and the line goes out on a saved copy of fd 1
     sys.stdout.flush()
@@ -272,6 +308,16 @@ def main():
         dist.init_process_group(BACKEND, rank=rank, world_size=world)
         if BACKEND == "gloo":
             local = 0
+    if args.launch_check:
+        joined = world
+        if dist:
+            t = torch.ones(1, dtype=torch.int64)
+            dist.all_reduce(t)  # gloo: host tensors
+            joined = int(t.item())
+            dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "ranks_joined": joined}), file=json_out, flush=True)
+        return
     torch.cuda.set_device(local)
     K = load_pkg()
     ctx = K.Context(local)
@@ -543,7 +589,7 @@ def main():
         log(extra_cfg["timeout"])
         emit()
         json_out.flush()
-        os._exit(0)
+        os._exit(3)  # the line is out, but a hung leg is a failure the launcher must see
 
     wd = None
     if args.legs_timeout > 0:
@@ -588,6 +634,8 @@ def main():
         def leg(*a):
             # a failing leg must not lose the headline line: a library failure on one rank aborts the
             # rank group, so every rank raises here and they stay in step
+            if os.environ.get("KGS_BENCH_FORCE_LEG_HANG"):  # test hook: a leg that never returns
+                time.sleep(1e9)
             try:
                 return large_leg(K, torch, dist, rank, world, local, *a, group)
             except Exception as e:

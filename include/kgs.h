@@ -91,13 +91,24 @@ int kgs_msm_combine(const uint8_t* T_all, int nparts, int c, uint8_t out_lem[64]
  * divisions on BLOCK slices with one all-gather of carries, and every MSM over the rank's slice of
  * the SRS. Each rank passes the FULL inputs (as for kgs_prove / kgs_prove_device) and receives the
  * identical, full proof (byte-identical to the single-GPU prover). Needs n >= 2 W^2.
- * All ranks must call the prover with the same arguments, in the same order.
+ * All ranks must call the prover with the same arguments, in the same order. Each rank may hold the
+ * whole SRS (kgs_srs_load_ptau: the MSMs read it with a point stride) or only its slice
+ * (kgs_srs_load_ptau_slice(ctx, path, nbits, rank, world): 1/world of the tables).
  * Transports:
  *   local : several contexts of ONE process (one host thread per rank; devices may differ)
  *   host  : any host all-gather callback (e.g. torch.distributed gloo); device data via the host
  *   rccl  : one process per GPU, RCCL over xGMI (rank 0 makes the id, the caller broadcasts it)
- * A rank failing with anything but a semantic prover error (not well calculated / not divisible /
- * does not divide / bad argument) aborts the group: the other ranks fail too, the group is spent. */
+ * Failures:
+ *   - rank-local preconditions (no / too small / wrong-slice SRS, pinned staging) are decided by all
+ *     ranks together before the first exchange: every rank fails with the lowest failing rank's
+ *     error and the group stays usable;
+ *   - semantic prover errors (not well calculated / not divisible / does not divide) are decided
+ *     from exchanged values, identically on every rank: the group stays usable;
+ *   - anything else (HIP, allocation, transport) aborts the group: local / host peers fail at their
+ *     next exchange; RCCL peers fail when their wait for the exchange passes the deadline
+ *     KGS_GROUP_TIMEOUT_S (default 120 s; ncclCommAbort alone does not release them). The group is
+ *     spent. The RCCL transport has run end to end with a one-rank communicator only (no multi-GPU
+ *     box was available to this build); local-group runs of up to 16 ranks cover the data path. */
 typedef struct kgs_group kgs_group_t;
 int kgs_group_create_local(int world, kgs_group_t** out);
 int kgs_group_create_host(int world, kgs_allgather_fn fn, void* user, kgs_group_t** out);
@@ -125,6 +136,15 @@ int kgs_ctx_set_msm_lanes(kgs_ctx_t* ctx, int lanes);
  * path, size and mtime) for a domain >= 2^nbits_max keeps them (no-op); tables of that file built
  * for a large enough domain by another context on the device are shared, not rebuilt. */
 int kgs_srs_load_ptau(kgs_ctx_t* ctx, const char* path, int nbits_max);
+/* A rank's slice of the SRS for the distributed prover (kgs_ctx_set_group, SURVEY.md §8e: "each GPU
+ * holds only its SRS slice"): of the first 2^(nbits_max+1) points only rank + world * j are read,
+ * made resident and window-expanded — 1/world of the tables of kgs_srs_load_ptau. Every MSM of the
+ * distributed prover runs over the rank's CYCLIC slice, whose scalar j multiplies exactly point
+ * rank + world * j, so this is all a rank needs. A context holding a slice proves only as that rank
+ * of a group of that world (kgs_prove on it alone fails with KGS_E_ARG). Same grow-only cache. */
+int kgs_srs_load_ptau_slice(kgs_ctx_t* ctx, const char* path, int nbits_max, int rank, int world);
+/* slice of the resident SRS (world 1: the whole prefix) and the bytes of its window tables */
+int kgs_srs_slice_info(kgs_ctx_t* ctx, int* rank, int* world, uint64_t* table_bytes);
 /* Power of a ptau file from its header only (readPTauHeader, src/ptau_utils.js:3-24). */
 int kgs_ptau_power(const char* path, int* power);
 /* Same from in-memory LEM points (npts >= 2). `power` is the ceremony power to report. */

@@ -53,6 +53,9 @@ def lib():
         L.kgs_ctx_destroy.argtypes = [ctypes.c_void_p]
         L.kgs_ctx_destroy.restype = None
         L.kgs_srs_load_ptau.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
+        L.kgs_srs_load_ptau_slice.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.kgs_srs_slice_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                         ctypes.POINTER(ctypes.c_uint64)]
         L.kgs_ptau_power.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
         L.kgs_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.kgs_srs_load_points.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
@@ -360,8 +363,19 @@ class Context:
         _check(lib().kgs_ctx_set_group(self._h, group._h if group is not None else None, rank))
         self._group = group
 
-    def load_ptau(self, path, nbits_max=-1):
-        _check(lib().kgs_srs_load_ptau(self._h, os.fsencode(path), nbits_max))
+    def load_ptau(self, path, nbits_max=-1, slice=None):
+        """kgs_srs_load_ptau; slice=(rank, world): only rank's slice of the SRS, the points rank + world*j
+        (kgs_srs_load_ptau_slice) — what a rank of the distributed prover commits with"""
+        if slice is None:
+            _check(lib().kgs_srs_load_ptau(self._h, os.fsencode(path), nbits_max))
+        else:
+            _check(lib().kgs_srs_load_ptau_slice(self._h, os.fsencode(path), nbits_max, int(slice[0]), int(slice[1])))
+
+    def srs_slice_info(self):
+        """(rank, world, window-table bytes) of the resident SRS (world 1: the whole prefix)"""
+        r, w, b = ctypes.c_int(), ctypes.c_int(), ctypes.c_uint64()
+        _check(lib().kgs_srs_slice_info(self._h, ctypes.byref(r), ctypes.byref(w), ctypes.byref(b)))
+        return r.value, w.value, b.value
         self._srs = (path, nbits_max)
 
     def srs_info(self):

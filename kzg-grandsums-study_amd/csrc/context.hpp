@@ -93,6 +93,9 @@ struct SrsTables {
   int device = 0;
   std::string file;  // file identity (path + size + mtime) or "mem#<id>"
   int power = -1, nbits_max = -1;
+  // a rank's slice of the SRS (kgs_srs_load_ptau_slice): row 0 holds the points slice_rank +
+  // slice_world * j only (slice_world == 1: the whole prefix)
+  int slice_rank = 0, slice_world = 1;
   MsmTables tb;
   ~SrsTables() {
     if (tb.table) {
@@ -122,7 +125,25 @@ extern std::vector<std::weak_ptr<DomainTables>> g_dom_reg;
 
 using namespace kgsi;
 
-struct kgs_group;  // rank group of the distributed prover (prover_dist.cpp)
+// Rank group of the distributed prover (transports in prover_dist.cpp). wait() drains a stream that
+// may hold the group's exchanges: a transport whose peers can hang (RCCL) polls it against a
+// deadline instead of blocking forever.
+struct kgs_group {
+  int world = 1;
+  virtual ~kgs_group() {}
+  // blocking host all-gather: recv = world x bytes, rank-major
+  virtual void allgather(int rank, const void* send, void* recv, size_t bytes) = 0;
+  // device all-to-all ordered on st: chunk j of send -> rank j; chunk j of recv <- rank j
+  virtual void alltoall(int rank, struct kgs_ctx& c, hipStream_t st, const void* send, void* recv, size_t chunk) = 0;
+  // a rank failed: unblock the others (they fail too instead of waiting forever)
+  virtual void abort() {}
+  virtual void wait(hipStream_t st) {
+    const hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) throw KgsError(KGS_E_HIP, std::string("HIP error: ") + hipGetErrorString(e) + " (stream sync)");
+  }
+};
+// seconds a rank waits for its peers in a group exchange (KGS_GROUP_TIMEOUT_S, default 120)
+double group_timeout_s();
 
 struct kgs_ctx {
   // every C-ABI entry point that touches the context holds mu: a busy context blocks its caller,
@@ -172,6 +193,7 @@ struct kgs_ctx {
   // distributed prover (kgs_ctx_set_group): every vector sharded over the group's ranks
   kgs_group* group = nullptr;
   int group_rank = 0;
+  int srs_slice_rank = 0, srs_slice_world = 1;  // of the loaded SRS (SrsTables::slice_*)
   std::map<std::string, uint32_t*> dist_tabs;  // per-rank coset / 1/(n(x-1)) tables (pool buffers)
 
   ~kgs_ctx() {
@@ -257,7 +279,8 @@ struct kgs_ctx {
     return d;
   }
   void sync() {
-    HC(hipStreamSynchronize(st));
+    if (group) group->wait(st);  // the main stream carries the group's exchanges
+    else HC(hipStreamSynchronize(st));
     if (st2) HC(hipStreamSynchronize(st2));
     if (st_copy) HC(hipStreamSynchronize(st_copy));
   }
@@ -271,6 +294,8 @@ struct kgs_ctx {
     tb = s ? s->tb : MsmTables{};
     srs_power = s ? s->power : -1;
     nbits_max = s ? s->nbits_max : -1;
+    srs_slice_rank = s ? s->slice_rank : 0;
+    srs_slice_world = s ? s->slice_world : 1;
   }
   void use_domain(const std::shared_ptr<DomainTables>& d) {
     dom = d;

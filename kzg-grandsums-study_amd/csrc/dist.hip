@@ -165,6 +165,23 @@ void launch_unpack_c2b(hipStream_t st, uint32_t* out, const uint32_t* recv, uint
   hipLaunchKernelGGL(k_unpack_c2b, dim3(nbk(Lb)), dim3(256), 0, st, out, recv, Lb, (uint32_t)W);
 }
 
+// BLOCK -> CYCLIC send side (the inverse of k_unpack_c2b): send[d c2 + t] = blk[d + W t]; rank d
+// receives from every source rank r the c2 = Lb / W elements r M + d + W t, i.e. its cyclic
+// positions r c2 + t, so the received buffer is the cyclic slice in natural order
+__global__ void __launch_bounds__(256) k_pack_b2c(uint32_t* __restrict__ send, const uint32_t* __restrict__ blk,
+                                                  uint64_t Lb, uint32_t W) {
+  KGS_AUX_PRIO();
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // position in send
+  if (p >= Lb) return;
+  const uint64_t c2 = Lb / W;
+  const uint64_t d = p / c2, t = p % c2;
+  fr::load(blk + 8 * (d + (uint64_t)W * t)).store(send + 8 * p);
+}
+
+void launch_pack_b2c(hipStream_t st, uint32_t* send, const uint32_t* blk, uint64_t Lb, int W) {
+  hipLaunchKernelGGL(k_pack_b2c, dim3(nbk(Lb)), dim3(256), 0, st, send, blk, Lb, (uint32_t)W);
+}
+
 // builder scan across ranks: the local builder left out[0] = local total and out[i] = local
 // exclusive scan (i >= 1); with off = the op-sum of the lower ranks' totals: out[0] = off,
 // out[i] = off (+|*) out[i]

@@ -93,6 +93,7 @@ void launch_dfwd_wdft(hipStream_t st, uint32_t* out, const uint32_t* recv, int l
 void launch_dinv_wdft_pack(hipStream_t st, uint32_t* send, const uint32_t* loc, int logMl, int W, int r,
                            const uint32_t* tw_inv, int logN);
 void launch_unpack_c2b(hipStream_t st, uint32_t* out, const uint32_t* recv, uint64_t Lb, int W);
+void launch_pack_b2c(hipStream_t st, uint32_t* send, const uint32_t* blk, uint64_t Lb, int W);
 void launch_scan_fix(hipStream_t st, bool prod, uint32_t* out, const uint32_t* off, uint64_t n);
 void launch_e_heads(hipStream_t st, uint32_t* heads, const uint32_t* S, uint64_t Ml, int W, int rot);
 void launch_quotient_e(hipStream_t st, bool prod, bool sel, uint32_t* q, const uint32_t* S, const uint32_t* F,

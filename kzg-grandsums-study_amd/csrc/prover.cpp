@@ -208,10 +208,26 @@ void ensure_msm_work(kgs_ctx& c) {
 }
 
 // Build (or share) the window tables of `npts` LEM points. `file` identifies the source; an empty
-// `file` (in-memory points) is never shared. The context's SRS is replaced only once the new tables
-// and the work buffers exist: a failed load leaves the context without an SRS ("no SRS loaded"),
-// never with a half-built one.
-void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int nbits_max, const std::string& file) {
+// `file` (in-memory points) is never shared. (srank, sworld): the points are a rank's slice of the
+// SRS (points srank + sworld * j of the file; sworld == 1: the prefix). The context's SRS is replaced
+// only once the new tables and the work buffers exist: a failed load leaves the context without an
+// SRS ("no SRS loaded"), never with a half-built one. The device registry lock is held only to look
+// up and to publish: the build (H2D copy + window expansion, seconds at 2^25 points) runs outside it,
+// so other contexts of the device are not blocked meanwhile; a concurrent build of the same tables
+// that published first wins and this one is dropped.
+static std::shared_ptr<SrsTables> srs_lookup(int device, const std::string& file, int nbits_max, int srank, int sworld) {
+  if (file.empty()) return nullptr;
+  for (auto& w : g_srs_reg) {
+    auto t = w.lock();
+    if (t && t->device == device && t->file == file && t->nbits_max >= nbits_max && t->slice_rank == srank &&
+        t->slice_world == sworld)
+      return t;
+  }
+  return nullptr;
+}
+
+void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int nbits_max, const std::string& file,
+                 int srank = 0, int sworld = 1) {
   if (npts < 2) throw KgsError(KGS_E_ARG, "SRS needs at least 2 points");
   c.sync();
   c.use_srs(nullptr);
@@ -219,45 +235,45 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
   std::shared_ptr<SrsTables> s;
   {
     std::lock_guard<std::mutex> lk(g_reg_mu);
-    if (!file.empty())
-      for (auto& w : g_srs_reg) {
-        auto t = w.lock();
-        if (t && t->device == c.device && t->file == file && t->nbits_max >= nbits_max) {
-          s = t;
-          break;
-        }
+    s = srs_lookup(c.device, file, nbits_max, srank, sworld);
+  }
+  if (!s) {
+    int cc = choose_c(npts);
+    int W = (255 + cc - 1) / cc;
+    // sorted entries pack j * npts + i into 31 bits (bit 31 = sign): widen the window until it fits
+    while ((uint64_t)W * npts > (1ull << 31) && cc < KGS_C_MAX) {
+      cc++;
+      W = (255 + cc - 1) / cc;
+    }
+    if ((uint64_t)W * npts > (1ull << 31)) throw KgsError(KGS_E_SRS, "SRS too large for the MSM entry index");
+    auto t = std::make_shared<SrsTables>();
+    t->device = c.device;
+    t->file = file;
+    t->power = power;
+    t->nbits_max = nbits_max;
+    t->slice_rank = srank;
+    t->slice_world = sworld;
+    t->tb.npts = npts;
+    t->tb.c = cc;
+    t->tb.W = W;
+    HC(dev_malloc((void**)&t->tb.table, (size_t)W * npts * 64));
+    HC(hipMemcpyAsync(t->tb.table, lem, npts * 64, hipMemcpyHostToDevice, c.st));
+    // build temporaries are released right after the build (they would otherwise stay in the pool)
+    struct Tmp {
+      void* p = nullptr;
+      ~Tmp() {
+        if (p) hipFree(p);
       }
-    if (!s) {
-      int cc = choose_c(npts);
-      int W = (255 + cc - 1) / cc;
-      // sorted entries pack j * npts + i into 31 bits (bit 31 = sign): widen the window until it fits
-      while ((uint64_t)W * npts > (1ull << 31) && cc < KGS_C_MAX) {
-        cc++;
-        W = (255 + cc - 1) / cc;
-      }
-      if ((uint64_t)W * npts > (1ull << 31)) throw KgsError(KGS_E_SRS, "SRS too large for the MSM entry index");
-      auto t = std::make_shared<SrsTables>();
-      t->device = c.device;
-      t->file = file;
-      t->power = power;
-      t->nbits_max = nbits_max;
-      t->tb.npts = npts;
-      t->tb.c = cc;
-      t->tb.W = W;
-      HC(dev_malloc((void**)&t->tb.table, (size_t)W * npts * 64));
-      HC(hipMemcpy(t->tb.table, lem, npts * 64, hipMemcpyHostToDevice));
-      // build temporaries are released right after the build (they would otherwise stay in the pool)
-      struct Tmp {
-        void* p = nullptr;
-        ~Tmp() {
-          if (p) hipFree(p);
-        }
-      } tmp, scr;
-      HC(dev_malloc(&tmp.p, npts * 128));
-      HC(dev_malloc(&scr.p, npts * 32));
-      msm_build_table(c.st, t->tb.table, npts, cc, W, (uint32_t*)tmp.p, (uint32_t*)scr.p);
-      check_launch();
-      HC(hipStreamSynchronize(c.st));
+    } tmp, scr;
+    HC(dev_malloc(&tmp.p, npts * 128));
+    HC(dev_malloc(&scr.p, npts * 32));
+    msm_build_table(c.st, t->tb.table, npts, cc, W, (uint32_t*)tmp.p, (uint32_t*)scr.p);
+    check_launch();
+    HC(hipStreamSynchronize(c.st));
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    if (auto other = srs_lookup(c.device, file, nbits_max, srank, sworld)) {
+      s = other;  // built concurrently by another context and published first: ours is released
+    } else {
       g_srs_reg.erase(std::remove_if(g_srs_reg.begin(), g_srs_reg.end(), [](auto& w) { return w.expired(); }),
                       g_srs_reg.end());
       if (!file.empty()) g_srs_reg.push_back(t);
@@ -306,7 +322,18 @@ Commit commit_launch_slice(kgs_ctx& c, const uint32_t* scalars, uint64_t count, 
   const int cc = c.tb.c;
   const int slots = c.msm_slots > 64 ? c.msm_slots : 64;
   if (slot >= slots) throw KgsError(KGS_E_ARG, "too many commitments in flight");
-  if (N > c.tb.npts || (count && pbase + pstride * (count - 1) >= c.tb.npts))
+  uint64_t cap = c.tb.npts;  // global points the resident SRS covers
+  if (c.srs_slice_world > 1) {
+    // a rank's SRS slice holds the points slice_rank + slice_world * j only: it serves exactly the
+    // commitments over this rank's CYCLIC slice, whose scalar j multiplies that point
+    if (count && (pstride != (uint64_t)c.srs_slice_world || pbase != (uint64_t)c.srs_slice_rank))
+      throw KgsError(KGS_E_ARG, "the loaded SRS slice (rank " + std::to_string(c.srs_slice_rank) + " of " +
+                                    std::to_string(c.srs_slice_world) + ") does not hold this commitment's points");
+    pbase = 0;
+    pstride = 1;
+    cap = (uint64_t)c.srs_slice_rank + (uint64_t)c.srs_slice_world * c.tb.npts;
+  }
+  if (N > cap || (count && pbase + pstride * (count - 1) >= c.tb.npts))
     throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
   uint32_t* dT = c.buf("msm_T", (size_t)slots * cc * 128) + (size_t)slot * cc * 32;
   cm.h_T = c.pin((size_t)cc * 128);
@@ -569,6 +596,8 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   const size_t E = 32 * n;
   if (nbits < 1) throw KgsError(KGS_E_ARG, "nbits must be >= 1");
   if (c.srs_power < 0) throw KgsError(KGS_E_ARG, "no SRS loaded");
+  if (c.srs_slice_world > 1)
+    throw KgsError(KGS_E_ARG, "this context holds a rank's SRS slice: it proves only as that rank of a group (kgs_ctx_set_group)");
   if (c.srs_power < nbits)
     throw KgsError(KGS_E_SRS, "The Powers of Tau file is not sufficiently large to commit the polynomials.");
   if (nbits > c.nbits_max) throw KgsError(KGS_E_SRS, "SRS loaded for a smaller maximum domain; reload with larger nbits_max");
@@ -967,9 +996,14 @@ int kgs_srs_load_points(kgs_ctx_t* ctx, const uint8_t* g1_lem, uint64_t npts, in
   API_END
 }
 
-int kgs_srs_load_ptau(kgs_ctx_t* ctx, const char* path, int nbits_max) {
-  API_BEGIN
+}  // extern "C"
+
+// ptau section 2 -> device tables: the first 2^(nbits_max+1) points, or (world > 1) rank's slice of
+// them, the points rank + world * j, read in chunks and subsampled on the host
+static void load_ptau_impl(kgs_ctx_t* ctx, const char* path, int nbits_max, int rank, int world) {
   if (!ctx || !path) throw KgsError(KGS_E_ARG, "NULL argument");
+  if (world < 1 || world > 16 || (world & (world - 1)) || rank < 0 || rank >= world)
+    throw KgsError(KGS_E_ARG, "SRS slice: world must be 1, 2, 4, 8 or 16 and 0 <= rank < world");
   CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
   FILE* f = fopen(path, "rb");
@@ -986,16 +1020,54 @@ int kgs_srs_load_ptau(kgs_ctx_t* ctx, const char* path, int nbits_max) {
   const char* rp = realpath(path, real) ? real : path;
   const std::string file = std::string(rp) + "#" + std::to_string((long long)stt.st_size) + "#" +
                            std::to_string((long long)stt.st_mtim.tv_sec) + "." + std::to_string((long long)stt.st_mtim.tv_nsec);
-  // grow-only: tables loaded for a larger domain of the same file serve every smaller proof
-  if (ctx->srs && ctx->srs->file == file && ctx->srs->nbits_max >= nbits_max) return KGS_OK;
+  // grow-only: tables loaded for a larger domain of the same file (and slice) serve every smaller proof
+  if (ctx->srs && ctx->srs->file == file && ctx->srs->nbits_max >= nbits_max && ctx->srs->slice_rank == rank &&
+      ctx->srs->slice_world == world)
+    return;
   uint64_t avail = info.s2_size / 64;
   if (avail < 2) throw KgsError(KGS_E_IO, std::string(path) + ": ptau has no tauG1 section");
   uint64_t need = 1ull << (nbits_max + 1);
   if (need > avail) need = avail;
-  std::vector<uint8_t> pts(need * 64);
-  if (fseeko(f, (off_t)info.s2_pos, SEEK_SET) || fread(pts.data(), 1, pts.size(), f) != pts.size())
-    throw KgsError(KGS_E_IO, "cannot read tauG1 section");
-  load_points(*ctx, pts.data(), need, info.power, nbits_max, file);
+  const uint64_t mine = need > (uint64_t)rank ? (need - rank + world - 1) / world : 0;  // points rank + world j < need
+  if (mine < 2) throw KgsError(KGS_E_ARG, "SRS slice needs at least 2 points");
+  std::vector<uint8_t> pts(mine * 64);
+  if (fseeko(f, (off_t)info.s2_pos, SEEK_SET)) throw KgsError(KGS_E_IO, "cannot read tauG1 section");
+  if (world == 1) {
+    if (fread(pts.data(), 1, pts.size(), f) != pts.size()) throw KgsError(KGS_E_IO, "cannot read tauG1 section");
+  } else {
+    const uint64_t CH = (uint64_t)world << 16;  // points per read
+    std::vector<uint8_t> buf(CH * 64);
+    uint64_t j = 0;
+    for (uint64_t p0 = 0; p0 < need; p0 += CH) {
+      const uint64_t cnt = need - p0 < CH ? need - p0 : CH;
+      if (fread(buf.data(), 1, cnt * 64, f) != cnt * 64) throw KgsError(KGS_E_IO, "cannot read tauG1 section");
+      for (uint64_t q = (uint64_t)rank; q < cnt; q += world) memcpy(&pts[64 * j++], &buf[64 * q], 64);
+    }
+  }
+  load_points(*ctx, pts.data(), mine, info.power, nbits_max, file, rank, world);
+}
+
+extern "C" {
+
+int kgs_srs_load_ptau(kgs_ctx_t* ctx, const char* path, int nbits_max) {
+  API_BEGIN
+  load_ptau_impl(ctx, path, nbits_max, 0, 1);
+  API_END
+}
+
+int kgs_srs_load_ptau_slice(kgs_ctx_t* ctx, const char* path, int nbits_max, int rank, int world) {
+  API_BEGIN
+  load_ptau_impl(ctx, path, nbits_max, rank, world);
+  API_END
+}
+
+int kgs_srs_slice_info(kgs_ctx_t* ctx, int* rank, int* world, uint64_t* table_bytes) {
+  API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  CTX_LOCK(ctx);
+  if (rank) *rank = ctx->srs_slice_rank;
+  if (world) *world = ctx->srs_slice_world;
+  if (table_bytes) *table_bytes = ctx->srs ? (uint64_t)ctx->tb.W * ctx->tb.npts * 64 : 0;
   API_END
 }
 
@@ -1476,7 +1548,7 @@ int kgs_bench_msm(kgs_ctx_t* ctx, const void* d_scalars_mont, uint64_t n, int re
   if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
   CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
-  if (n > ctx->tb.npts) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
+  if (n > ctx->tb.npts || ctx->srs_slice_world > 1) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS (or an SRS slice)");
   uint32_t* dT = ctx->buf("msm_T", (size_t)64 * ctx->tb.c * 128);
   msm_run(ctx->st, ctx->tb, ctx->mw, (const uint32_t*)d_scalars_mont, n, dT);  // warm
   hipEvent_t e0, e1;
@@ -1500,7 +1572,7 @@ int kgs_bench_msm_phases(kgs_ctx_t* ctx, const void* d_scalars_mont, uint64_t n,
   if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
   CTX_LOCK(ctx);
   HC(hipSetDevice(ctx->device));
-  if (n > ctx->tb.npts) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS");
+  if (n > ctx->tb.npts || ctx->srs_slice_world > 1) throw KgsError(KGS_E_SRS, "MSM larger than the resident SRS (or an SRS slice)");
   uint32_t* dT = ctx->buf("msm_T", (size_t)64 * ctx->tb.c * 128);
   hipEvent_t ev[5];
   for (auto& e : ev) HC(hipEventCreate(&e));

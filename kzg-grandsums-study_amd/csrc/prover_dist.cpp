@@ -24,6 +24,7 @@
 // one process: tests on one GPU, or one process driving several GPUs), host callback (any
 // all-gather, e.g. torch.distributed gloo; device data staged through the host).
 #include <condition_variable>
+#include <thread>
 #include <rccl/rccl.h>
 
 #include "context.hpp"
@@ -33,16 +34,15 @@ using namespace kgs;
 using namespace kgsi;
 
 // ------------------------------------------------------------------ rank groups
-struct kgs_group {
-  int world = 1;
-  virtual ~kgs_group() {}
-  // blocking host all-gather: recv = world x bytes, rank-major
-  virtual void allgather(int rank, const void* send, void* recv, size_t bytes) = 0;
-  // device all-to-all ordered on st: chunk j of send -> rank j; chunk j of recv <- rank j
-  virtual void alltoall(int rank, kgs_ctx& c, hipStream_t st, const void* send, void* recv, size_t chunk) = 0;
-  // a rank failed: unblock the others (they fail too instead of waiting forever)
-  virtual void abort() {}
-};
+// (the kgs_group interface is in context.hpp: kgs_ctx::sync drains the main stream through it)
+double group_timeout_s() {
+  static const double t = [] {
+    const char* e = getenv("KGS_GROUP_TIMEOUT_S");
+    const double v = e ? atof(e) : 0.0;
+    return v > 0 ? v : 120.0;
+  }();
+  return t;
+}
 
 namespace {
 
@@ -68,7 +68,7 @@ struct LocalGroup : kgs_group {
       cv.notify_all();
       return;
     }
-    if (!cv.wait_for(lk, std::chrono::seconds(600), [&] { return gen != g || broken; })) {
+    if (!cv.wait_for(lk, std::chrono::duration<double>(group_timeout_s()), [&] { return gen != g || broken; })) {
       broken = true;
       cv.notify_all();
       throw KgsError(KGS_E_COMM, "rank group barrier timed out");
@@ -144,6 +144,7 @@ struct RcclGroup : kgs_group {
   }
   void allgather(int rank, const void* send, void* recv, size_t bytes) override {
     HC(hipSetDevice(device));
+    if (!comm) throw KgsError(KGS_E_COMM, "rank group aborted");
     if (small_bytes < bytes * (world + 1)) {
       if (d_small) HC(hipFree(d_small));
       d_small = nullptr;
@@ -155,10 +156,34 @@ struct RcclGroup : kgs_group {
     HC(hipMemcpyAsync(ds, send, bytes, hipMemcpyHostToDevice, st_small));
     NC(ncclAllGather(ds, ds + bytes, bytes, ncclUint8, comm, st_small));
     HC(hipMemcpyAsync(recv, ds + bytes, bytes * world, hipMemcpyDeviceToHost, st_small));
-    HC(hipStreamSynchronize(st_small));
+    wait(st_small);
     (void)rank;
   }
+  // RCCL collectives are stream-ordered: a peer that never joins leaves the stream pending forever
+  // (and ncclCommAbort on the failing rank does not release the others). Poll the stream and the
+  // communicator's asynchronous error against the group deadline; on expiry or error abort this
+  // rank's communicator too and fail, so every rank of a broken group ends with an error.
+  void wait(hipStream_t st) override {
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(group_timeout_s());
+    for (unsigned spin = 0;; spin++) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) return;
+      if (q != hipErrorNotReady) throw KgsError(KGS_E_HIP, std::string("HIP error: ") + hipGetErrorString(q) + " (stream query)");
+      ncclResult_t ae = ncclSuccess;
+      if (comm && ncclCommGetAsyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+        abort();
+        throw KgsError(KGS_E_COMM, std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae));
+      }
+      if (!comm) throw KgsError(KGS_E_COMM, "rank group aborted");
+      if (std::chrono::steady_clock::now() > t_end) {
+        abort();
+        throw KgsError(KGS_E_COMM, "rank group exchange timed out (a peer rank failed or hung; KGS_GROUP_TIMEOUT_S)");
+      }
+      if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
   void alltoall(int, kgs_ctx&, hipStream_t st, const void* send, void* recv, size_t chunk) override {
+    if (!comm) throw KgsError(KGS_E_COMM, "rank group aborted");
     NC(ncclGroupStart());
     for (int j = 0; j < world; j++) {
       NC(ncclSend((const uint8_t*)send + (size_t)j * chunk, chunk, ncclUint8, j, comm, st));
@@ -240,6 +265,14 @@ struct Dist {
     check_launch();
   }
   void block_to_e(uint32_t* outE, const uint32_t* inB, uint64_t Ml) { a2a(inB, outE, Ml / W); }
+  // BLOCK -> CYCLIC (the inverse of cyc_to_block): send chunk d = the block's indices = d mod W; the
+  // received chunks, in source-rank order, are the cyclic slice in natural order
+  void block_to_cyc(uint32_t* outC, const uint32_t* inB, uint64_t Lb) {
+    uint32_t* send = c.buf("d_send", 32 * Lb);
+    launch_pack_b2c(c.st, send, inB, Lb, W);
+    check_launch();
+    a2a(send, outC, Lb / W);
+  }
   void cyc_to_block(uint32_t* outB, const uint32_t* inC, uint64_t Lb) {
     uint32_t* recv = c.buf("d_recv", 32 * Lb);
     a2a(inC, recv, Lb / W);
@@ -268,6 +301,54 @@ struct Dist {
 
 }  // namespace
 
+// Rank-local preconditions (SRS loaded and large enough, the loaded SRS slice matching this rank,
+// pinned staging): a rank failing one of them must not leave its peers waiting in the first
+// exchange, so every rank decides them together — one all-gather of each rank's first failure, and
+// every rank throws the lowest failing rank's error (the group stays usable: nothing was exchanged).
+void dist_preconditions(kgs_ctx& c, const ProveIn& in) {
+  const int W = c.group->world, r = c.group_rank;
+  struct Verdict {
+    int32_t code;
+    char msg[252];
+  } mine{};
+  try {
+    const int nbits = in.nbits, k = in.npols;
+    const int logW = ilog2(W);
+    if ((1 << logW) != W || W > 16) throw KgsError(KGS_E_ARG, "distributed prover: world must be 1, 2, 4, 8 or 16");
+    if (nbits < 2 * logW + 1) throw KgsError(KGS_E_ARG, "distributed prover: domain too small for the group (need n >= 2 W^2)");
+    if (c.srs_power < 0) throw KgsError(KGS_E_ARG, "no SRS loaded");
+    if (c.srs_power < nbits)
+      throw KgsError(KGS_E_SRS, "The Powers of Tau file is not sufficiently large to commit the polynomials.");
+    if (nbits > c.nbits_max) throw KgsError(KGS_E_SRS, "SRS loaded for a smaller maximum domain; reload with larger nbits_max");
+    if (c.srs_slice_world > 1 && (c.srs_slice_world != W || c.srs_slice_rank != r))
+      throw KgsError(KGS_E_ARG, "the loaded SRS slice (rank " + std::to_string(c.srs_slice_rank) + " of " +
+                                    std::to_string(c.srs_slice_world) + ") is not this context's (rank " + std::to_string(r) +
+                                    " of " + std::to_string(W) + ")");
+    if (k < 1) throw KgsError(KGS_E_ARG, "The number of multisets must be greater than 0.");
+    if (k > KGS_MAX_POLS) throw KgsError(KGS_E_ARG, "too many multisets");
+    const uint64_t M = (1ull << nbits) / W;
+    const int ncom_all = 2 * k + (in.sel_f ? 2 : 0) + 4;
+    c.msm_slots = ncom_all + 4;
+    c.ensure_pin(((size_t)ncom_all + 8) * ((size_t)c.tb.c * 128 + 64) +
+                 32 * (size_t)((M + EVAL_TILE - 1) / EVAL_TILE) * (2 * k + 8) + ((size_t)kgs_ctx::SCAL_BYTES * 2) +
+                 (8 << 20));
+  } catch (const KgsError& e) {
+    mine.code = e.code;
+    snprintf(mine.msg, sizeof(mine.msg), "%s", e.what());
+  } catch (const std::exception& e) {
+    mine.code = KGS_E_HIP;
+    snprintf(mine.msg, sizeof(mine.msg), "%s", e.what());
+  }
+  std::vector<Verdict> all(W);
+  c.group->allgather(r, &mine, all.data(), sizeof(Verdict));
+  for (int j = 0; j < W; j++)
+    if (all[j].code != KGS_OK) {
+      all[j].msg[sizeof(all[j].msg) - 1] = 0;
+      throw KgsError(all[j].code, j == r ? std::string(all[j].msg)
+                                         : std::string(all[j].msg) + " (on rank " + std::to_string(j) + ")");
+    }
+}
+
 void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out) {
   using clk = std::chrono::steady_clock;
   auto t0 = clk::now();
@@ -289,20 +370,10 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
   const int k = in.npols;
   const int nbits = in.nbits;
   const uint64_t n = 1ull << nbits;
-  if ((1 << logW) != W || W > 16) throw KgsError(KGS_E_ARG, "distributed prover: world must be 1, 2, 4, 8 or 16");
-  if (nbits < 2 * logW + 1) throw KgsError(KGS_E_ARG, "distributed prover: domain too small for the group (need n >= 2 W^2)");
-  if (c.srs_power < 0) throw KgsError(KGS_E_ARG, "no SRS loaded");
-  if (c.srs_power < nbits)
-    throw KgsError(KGS_E_SRS, "The Powers of Tau file is not sufficiently large to commit the polynomials.");
-  if (nbits > c.nbits_max) throw KgsError(KGS_E_SRS, "SRS loaded for a smaller maximum domain; reload with larger nbits_max");
-  if (k < 1) throw KgsError(KGS_E_ARG, "The number of multisets must be greater than 0.");
-  if (k > KGS_MAX_POLS) throw KgsError(KGS_E_ARG, "too many multisets");
+  (void)logW;  // preconditions: dist_preconditions (decided by every rank together)
   const uint64_t M = n / W;  // local length of an n-vector in every layout
   const size_t EM = 32 * M;
   const int ncom_all = 2 * k + (sel ? 2 : 0) + 4;
-  c.msm_slots = ncom_all + 4;
-  c.ensure_pin(((size_t)ncom_all + 8) * ((size_t)c.tb.c * 128 + 64) + 32 * (size_t)((M + EVAL_TILE - 1) / EVAL_TILE) *
-                   (2 * k + 8) + ((size_t)kgs_ctx::SCAL_BYTES * 2) + (8 << 20));
   c.reset_staging();
   uint32_t* flags = c.buf("flags", 64);
   HC(hipMemsetAsync(flags, 0, 64, c.st));
@@ -355,11 +426,6 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
   auto commit_cyc = [&](const uint32_t* sc, uint64_t N) {
     const uint64_t cnt = N > (uint64_t)r ? (N - r + W - 1) / W : 0;
     return commit_launch_slice(c, sc, cnt, (uint64_t)r, (uint64_t)W, N, slot++, 0);
-  };
-  // BLOCK slice [lo, lo + len) of a polynomial with N points
-  auto commit_blk = [&](const uint32_t* sc, uint64_t lo, uint64_t len, uint64_t N) {
-    const uint64_t cnt = N > lo ? std::min(len, N - lo) : 0;
-    return commit_launch_slice(c, sc, cnt, lo, 1, N, slot++, 0);
   };
   std::vector<Commit> r1;
   for (int i = 0; i < k; i++) {
@@ -665,8 +731,14 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
   launch_div_fix(c.st, WxB, pz1, d_cc, Mc);
   launch_div_fix(c.st, W2B, pz2, d_cc + 8, M);
   check_launch();
-  Commit cW1 = commit_blk(WxB, (uint64_t)r * Mc, Mc, L - 1);
-  Commit cW2 = commit_blk(W2B, (uint64_t)r * M, M, n - 1);
+  // the openings go back to CYCLIC (one all-to-all each), so that every MSM of the proof reads the
+  // same per-rank SRS slice (points r + W j: kgs_srs_load_ptau_slice)
+  uint32_t* WxC = c.buf("d_WxC", 32 * Mc);
+  uint32_t* W2C = c.buf("d_W2C", EM);
+  D.block_to_cyc(WxC, WxB, Mc);
+  D.block_to_cyc(W2C, W2B, M);
+  Commit cW1 = commit_cyc(WxC, L - 1);
+  Commit cW2 = commit_cyc(W2C, n - 1);
   c.sync();
   commits_finish_with(c, {cW1, cW2}, {com[ci].data(), com[ci + 1].data()}, W, D.host_ag());
   ci += 2;
@@ -677,14 +749,17 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
   c.reset_staging();
 }
 
-// semantic failures (same inputs -> same decision on every rank) leave the group usable; anything
-// else aborts it so that the other ranks fail instead of waiting in a collective
+// Preconditions are agreed by all ranks (dist_preconditions: they all throw together, the group
+// stays usable); semantic failures (decided from all-gathered values: the same on every rank) leave
+// the group usable too; anything else happened on this rank alone mid-proof and aborts the group, so
+// that the other ranks fail at their next exchange instead of waiting in it (RCCL: at the
+// KGS_GROUP_TIMEOUT_S deadline of RcclGroup::wait).
 void prove_dist_group(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out) {
+  dist_preconditions(c, in);
   try {
     prove_dist_impl(c, in, com_out, ev_out);
   } catch (const KgsError& e) {
-    if (e.code != KGS_E_NOT_WELL_CALC && e.code != KGS_E_NOT_DIVISIBLE && e.code != KGS_E_DOES_NOT_DIVIDE &&
-        e.code != KGS_E_ARG && e.code != KGS_E_SRS)
+    if (e.code != KGS_E_NOT_WELL_CALC && e.code != KGS_E_NOT_DIVISIBLE && e.code != KGS_E_DOES_NOT_DIVIDE)
       c.group->abort();
     throw;
   } catch (...) {

@@ -10,6 +10,7 @@
 #include <chrono>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/kgs.h"
@@ -276,7 +277,8 @@ struct Job {
   napi_async_work work = nullptr;
   napi_deferred deferred = nullptr;
   kgs_ctx_t* ctx = nullptr;
-  int op = 0;  // 0 = load ptau, 1 = prove, 2 = elementwise Fr map / transform (frOp)
+  int op = 0;  // 0 = load ptau, 1 = prove, 2 = elementwise Fr map / transform (frOp),
+               // 3 = one distributed proof over a rank group (proveGroup), 4 = msmPoints
   int rc = 0;
   std::string err;
   // load
@@ -292,12 +294,95 @@ struct Job {
   bool selected = false;
   bool want_mont = true;  // false: no Montgomery write-back (the other ranks of a distributed proof)
   double exec_ms = 0;     // wall time of job_execute (the libkgs call on the worker thread)
+  // proveGroup: rank r's context, SRS slice r of W, one native thread per rank
+  std::vector<kgs_ctx_t*> ranks;
+  // msmPoints: bases and standard-form scalars (copied: the call returns before the work runs)
+  std::vector<uint8_t> bases, scal;
+  uint8_t msm_out[64];
   // frOp
   int fr_op = 0;
   View in;
   uint8_t* out = nullptr;  // out_alloc'd, adopted by JS on success
   size_t out_len = 0;
 };
+
+static void prove_one(Job* j, kgs_ctx_t* ctx, bool mont, std::vector<uint8_t>& com, std::vector<uint8_t>& ev, int& rc,
+                      std::string& err) {
+  int nc = 0, ne = 0;
+  kgs_proof_shape(j->kind, j->npols, j->selected ? 1 : 0, &nc, &ne);
+  com.resize(64 * (size_t)nc);
+  ev.resize(32 * (size_t)ne);
+  std::vector<const uint8_t*> fp, tp;
+  for (int i = 0; i < j->npols; i++) {
+    fp.push_back(j->f[i].p);
+    tp.push_back(j->t[i].p);
+  }
+  rc = kgs_prove(ctx, j->kind, j->nbits, j->npols, fp.data(), tp.data(), j->selected ? j->sf.p : nullptr,
+                 j->selected ? j->st.p : nullptr, mont ? j->mf.data() : nullptr, mont ? j->mt.data() : nullptr,
+                 com.data(), ev.data());
+  if (rc != KGS_OK) err = kgs_last_error();
+}
+
+// the inputs' shape, and (want_mont) the output buffers of the Montgomery write-back
+static bool prepare_prove(Job* j) {
+  const size_t E = (size_t)32 << j->nbits;
+  bool ok = true;
+  for (int i = 0; i < j->npols; i++) {
+    ok &= j->f[i].len == E && j->t[i].len == E;
+    if (j->want_mont) {
+      j->mf.push_back(out_alloc(E));
+      j->mt.push_back(out_alloc(E));
+      ok &= j->mf.back() && j->mt.back();
+    }
+  }
+  if (j->selected) ok &= j->sf.len == E && j->st.len == E;
+  if (!ok) {
+    j->rc = KGS_E_ARG;
+    j->err = "evaluation buffers must hold 2^nbits 32-byte elements";
+  }
+  return ok;
+}
+
+// One distributed proof: every rank on its own native thread (the group's barriers join them), so
+// the ranks never compete with each other — or with the context pool's proofs — for libuv's
+// thread pool (a rank waiting at a barrier for a rank that never got a pool thread would stall).
+// Each rank first makes its SRS slice resident (kgs_srs_load_ptau_slice: points r + W j), then
+// proves; rank 0 returns the proof and the Montgomery write-back, every rank's proof must agree.
+static void group_execute(Job* j) {
+  const int W = (int)j->ranks.size();
+  std::vector<int> rc(W, KGS_OK);
+  std::vector<std::string> err(W);
+  std::vector<std::vector<uint8_t>> com(W), ev(W);
+  std::vector<std::thread> th;
+  for (int r = 0; r < W; r++)
+    th.emplace_back([&, r] {
+      rc[r] = kgs_srs_load_ptau_slice(j->ranks[r], j->path.c_str(), j->nbits, r, W);
+      if (rc[r] != KGS_OK) err[r] = kgs_last_error();
+      // a rank whose load failed still enters the prover: the group agrees on the failure there
+      int rp = KGS_OK;
+      std::string ep;
+      prove_one(j, j->ranks[r], r == 0 && j->want_mont, com[r], ev[r], rp, ep);
+      if (rc[r] == KGS_OK) {
+        rc[r] = rp;
+        err[r] = ep;
+      }
+    });
+  for (auto& t : th) t.join();
+  for (int r = 0; r < W; r++)
+    if (rc[r] != KGS_OK) {
+      j->rc = rc[r];
+      j->err = err[r];
+      return;
+    }
+  for (int r = 1; r < W; r++)
+    if (com[r] != com[0] || ev[r] != ev[0]) {
+      j->rc = KGS_E_COMM;
+      j->err = "ranks of the distributed proof disagree";
+      return;
+    }
+  j->com = com[0];
+  j->ev = ev[0];
+}
 
 static void job_execute(napi_env, void* data) {
   Job* j = (Job*)data;
@@ -326,33 +411,23 @@ static void job_execute(napi_env, void* data) {
       case 2: j->rc = kgs_fr_batch_inverse(j->ctx, j->in.p, j->out, n); break;
       default: j->rc = kgs_ntt(j->ctx, j->in.p, j->out, logm, j->fr_op == 4); break;
     }
+  } else if (j->op == 3) {
+    if (prepare_prove(j)) group_execute(j);
+    return;
+  } else if (j->op == 4) {
+    const uint64_t n = j->scal.size() / 32;
+    int lg = 0;
+    while ((1ull << (lg + 1)) < n) lg++;
+    std::vector<uint8_t> mont(j->scal.size());
+    j->rc = kgs_srs_load_points(j->ctx, j->bases.data(), n, lg, lg);
+    if (j->rc == KGS_OK) j->rc = kgs_fr_to_mont(j->ctx, j->scal.data(), mont.data(), n);
+    if (j->rc == KGS_OK) j->rc = kgs_msm(j->ctx, mont.data(), n, j->msm_out);
   } else {
-    int nc = 0, ne = 0;
-    kgs_proof_shape(j->kind, j->npols, j->selected ? 1 : 0, &nc, &ne);
-    j->com.resize(64 * (size_t)nc);
-    j->ev.resize(32 * (size_t)ne);
-    std::vector<const uint8_t*> fp, tp;
-    const size_t E = (size_t)32 << j->nbits;
-    bool ok = true;
-    for (int i = 0; i < j->npols; i++) {
-      ok &= j->f[i].len == E && j->t[i].len == E;
-      fp.push_back(j->f[i].p);
-      tp.push_back(j->t[i].p);
-      if (j->want_mont) {
-        j->mf.push_back(out_alloc(E));
-        j->mt.push_back(out_alloc(E));
-        ok &= j->mf.back() && j->mt.back();
-      }
-    }
-    if (j->selected) ok &= j->sf.len == E && j->st.len == E;
-    if (!ok) {
-      j->rc = KGS_E_ARG;
-      j->err = "evaluation buffers must hold 2^nbits 32-byte elements";
-      return;
-    }
-    j->rc = kgs_prove(j->ctx, j->kind, j->nbits, j->npols, fp.data(), tp.data(), j->selected ? j->sf.p : nullptr,
-                      j->selected ? j->st.p : nullptr, j->want_mont ? j->mf.data() : nullptr,
-                      j->want_mont ? j->mt.data() : nullptr, j->com.data(), j->ev.data());
+    if (!prepare_prove(j)) return;
+    std::string e;
+    prove_one(j, j->ctx, j->want_mont, j->com, j->ev, j->rc, e);
+    if (j->rc != KGS_OK) j->err = e;
+    return;
   }
   if (j->rc != KGS_OK) j->err = kgs_last_error();
 }
@@ -373,6 +448,8 @@ static void job_complete(napi_env env, napi_status, void* data) {
   } else if (j->op == 2) {
     napi_resolve_deferred(env, j->deferred, adopt_u8(env, j->out, j->out_len));
     j->out = nullptr;
+  } else if (j->op == 4) {
+    napi_resolve_deferred(env, j->deferred, make_u8(env, j->msm_out, 64));
   } else {
     napi_value o, arr;
     napi_create_object(env, &o);
@@ -413,7 +490,7 @@ static napi_value queue(napi_env env, Job* j, const char* name) {
   napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &rname);
   NAPI_CALL(env, napi_create_async_work(env, nullptr, rname, job_execute, job_complete, j, &j->work));
   NAPI_CALL(env, napi_queue_async_work(env, j->work));
-  if (j->op == 1) flush_external(env);  // a GC it starts now runs beside the proof just queued
+  if (j->op == 1 || j->op == 3) flush_external(env);  // a GC it starts now runs beside the proof just queued
   return promise;
 }
 
@@ -436,6 +513,7 @@ static napi_value SrsLoad(napi_env env, napi_callback_info info) {
 
 // prove(ctx, kind, nbits, [F...], [T...], selF|null, selT|null[, wantMont = true])
 //   -> Promise<{commitments, evaluations, montF, montT}> (montF/montT empty without wantMont)
+static napi_value prove_args(napi_env env, napi_value* argv, size_t argc, Job* j);
 static napi_value Prove(napi_env env, napi_callback_info info) {
   size_t argc = 8;
   napi_value argv[8];
@@ -443,6 +521,43 @@ static napi_value Prove(napi_env env, napi_callback_info info) {
   Job* j = new Job();
   j->op = 1;
   j->ctx = get_ctx(env, argv[0]);
+  return prove_args(env, argv, argc, j);
+}
+
+// proveGroup([ctx_0..ctx_{W-1}], ptauPath, kind, nbits, [F...], [T...], selF|null, selT|null)
+//   -> Promise<{commitments, evaluations, montF, montT}>: one proof over the contexts' rank group
+//   (ctxSetGroup(ctx_r, group, r) beforehand), each rank with its SRS slice, one thread per rank
+static napi_value ProveGroup(napi_env env, napi_callback_info info) {
+  size_t argc = 8;
+  napi_value argv[8];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Job* j = new Job();
+  j->op = 3;
+  uint32_t W = 0;
+  napi_get_array_length(env, argv[0], &W);
+  for (uint32_t r = 0; r < W; r++) {
+    napi_value e;
+    napi_get_element(env, argv[0], r, &e);
+    j->ranks.push_back(get_ctx(env, e));
+  }
+  size_t len = 0;
+  napi_get_value_string_utf8(env, argv[1], nullptr, 0, &len);
+  j->path.resize(len + 1);
+  napi_get_value_string_utf8(env, argv[1], &j->path[0], len + 1, &len);
+  j->path.resize(len);
+  if (W < 1) {
+    delete j;
+    napi_throw_error(env, nullptr, "proveGroup: no ranks");
+    return nullptr;
+  }
+  // the prove(...) argument list from `kind` on: argv[2..7] -> positions 1..6 (argv[0] unused)
+  napi_value pa[8];
+  pa[0] = argv[0];
+  for (int i = 2; i < 8; i++) pa[i - 1] = argv[i];
+  return prove_args(env, pa, argc - 1, j);
+}
+
+static napi_value prove_args(napi_env env, napi_value* argv, size_t argc, Job* j) {
   napi_get_value_int32(env, argv[1], &j->kind);
   napi_get_value_int32(env, argv[2], &j->nbits);
   uint32_t nf = 0, nt = 0;
@@ -467,7 +582,7 @@ static napi_value Prove(napi_env env, napi_callback_info info) {
     napi_typeof(env, argv[7], &ty);
     if (ty == napi_boolean) napi_get_value_bool(env, argv[7], &j->want_mont);
   }
-  return queue(env, j, "kgs_prove");
+  return queue(env, j, j->op == 3 ? "kgs_prove_group" : "kgs_prove");
 }
 
 // frOp(ctx, op, Uint8Array) -> Promise<Uint8Array> on ctx's GPU, elementwise over 32 B elements:
@@ -605,30 +720,26 @@ static napi_value PairingEq(napi_env env, napi_callback_info info) {
   return out;
 }
 
-// msmPoints(ctx, bases, scalarsStd) -> 64 B affine LEM sum_i s_i P_i on the GPU of ctx (the
+// msmPoints(ctx, bases, scalarsStd) -> Promise<64 B affine LEM sum_i s_i P_i> on the GPU of ctx (the
 // curve shim's G1.multiExpAffine, polynomial.js:1112, whose scalars are standard-form LE after
-// Fr.batchFromMontgomery): the bases become ctx's resident point set
+// Fr.batchFromMontgomery): the bases become ctx's resident point set. Async work like every other
+// heavy call: the window-table build of the bases must not block the event loop.
 static napi_value MsmPoints(napi_env env, napi_callback_info info) {
   size_t argc = 3;
   napi_value argv[3];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
-  kgs_ctx_t* ctx = get_ctx(env, argv[0]);
-  std::vector<uint8_t> bases = bytes_of(env, argv[1]), sc = bytes_of(env, argv[2]);
-  const uint64_t n = sc.size() / 32;
-  if (sc.size() % 32 || bases.size() != 64 * n || n < 2) {
+  Job* j = new Job();
+  j->op = 4;
+  j->ctx = get_ctx(env, argv[0]);
+  j->bases = bytes_of(env, argv[1]);
+  j->scal = bytes_of(env, argv[2]);
+  const uint64_t n = j->scal.size() / 32;
+  if (j->scal.size() % 32 || j->bases.size() != 64 * n || n < 2) {
+    delete j;
     napi_throw_error(env, nullptr, "msmPoints: expected n >= 2 affine LEM bases and n 32 B scalars");
     return nullptr;
   }
-  int lg = 0;
-  while ((1ull << (lg + 1)) < n) lg++;
-  uint8_t out[64];
-  std::vector<uint8_t> mont(sc.size());
-  if (kgs_srs_load_points(ctx, bases.data(), n, lg, lg) != KGS_OK ||
-      kgs_fr_to_mont(ctx, sc.data(), mont.data(), n) != KGS_OK || kgs_msm(ctx, mont.data(), n, out) != KGS_OK) {
-    napi_throw_error(env, nullptr, kgs_last_error());
-    return nullptr;
-  }
-  return make_u8(env, out, 64);
+  return queue(env, j, "kgs_msm_points");
 }
 
 // lastTiming(ctx) -> [round 1..5 ms, -, input copy, prover, write-back wait] of the context's last
@@ -664,6 +775,7 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"groupCreateLocal", nullptr, GroupCreateLocal, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"ctxSetGroup", nullptr, CtxSetGroup, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"msmPoints", nullptr, MsmPoints, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"proveGroup", nullptr, ProveGroup, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"lastTiming", nullptr, LastTiming, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"ctxSetMsmLanes", nullptr, CtxSetMsmLanes, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"frOp", nullptr, FrOp, nullptr, nullptr, nullptr, napi_default, nullptr},

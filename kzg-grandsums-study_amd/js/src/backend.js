@@ -118,10 +118,12 @@ async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT) {
 // proof of at least 2^KGS_JS_SHARD_MIN_NBITS elements (default 22) runs on W contexts (rank r on
 // device r mod #devices) joined by an in-process rank group (kgs_group_create_local +
 // kgs_ctx_set_group): every vector of the proof sharded, NTTs as rank-local transforms plus one
-// all-to-all, every MSM over a per-rank slice of the SRS (DESIGN.md §6). The W ranks run as
-// concurrent async jobs on the libuv pool and all produce the same proof; rank 0 also returns the
-// Montgomery write-back. One sharded proof at a time (the group's barriers join the ranks of one
-// proof); the same inputs and the same Promise result as the single-GPU path.
+// all-to-all, every MSM over the rank's slice of the SRS, which is all a rank loads
+// (kgs_srs_load_ptau_slice; DESIGN.md §6). The W ranks run as ONE async job that starts one native
+// thread per rank (addon proveGroup), so they never wait for libuv pool threads held by other work;
+// rank 0 returns the proof and the Montgomery write-back. One sharded proof at a time (the group's
+// barriers join the ranks of one proof); the same inputs and the same Promise result as the
+// single-GPU path.
 const shard = { ctxs: null, group: null, busy: Promise.resolve() };
 function shardRanks() {
     const v = parseInt(process.env.KGS_JS_SHARD_RANKS || "0", 10);
@@ -144,11 +146,8 @@ function proveSharded(kind, key, nBits, evalsF, evalsT, selF, selT) {
             shard.group = a.groupCreateLocal(W);
             shard.ctxs.forEach((c, r) => a.ctxSetGroup(c, shard.group, r));
         }
-        await Promise.all(shard.ctxs.map(c => a.srsLoadPtau(c, key, nBits)));
         try {
-            const res = await Promise.all(shard.ctxs.map((c, r) =>
-                a.prove(c, kind, nBits, evalsF, evalsT, selF, selT, r === 0)));
-            return res[0];
+            return await a.proveGroup(shard.ctxs, key, kind, nBits, evalsF, evalsT, selF, selT);
         } catch (e) {
             // a rank failed: the group may be spent (the others were released with an error); make a
             // fresh one for the next proof

@@ -218,7 +218,12 @@ function buildG1(F1, Fr, addon) {
                 return encJ(R);
             }
             const a = addon();
-            return encJ(dec(a.msmPoints(shimContext(a), bases.subarray(0, 64 * n), scalars.subarray(0, 32 * n))));
+            // async on a libuv thread (the bases' window tables are built there, not on the event
+            // loop); the shim context's point set is per call, so its MSMs run one at a time
+            const run = () => a.msmPoints(shimContext(a), bases.subarray(0, 64 * n), scalars.subarray(0, 32 * n));
+            const p = shimBusy.then(run, run);
+            shimBusy = p.catch(() => {});
+            return encJ(dec(await p));
         },
     };
     return G1;
@@ -226,6 +231,7 @@ function buildG1(F1, Fr, addon) {
 
 // one context of its own for the shim's MSMs (its point set is replaced by every call)
 let shimCtx = null;
+let shimBusy = Promise.resolve();
 function shimContext(a) {
     if (!shimCtx) shimCtx = a.ctxCreate(0);
     return shimCtx;

@@ -146,6 +146,16 @@ def cyclic_to_block(cyc, W):
     return out
 
 
+def block_to_cyclic(blocks, W):
+    """BLOCK -> CYCLIC (the openings before their commitment MSMs): rank r sends chunk d = its block's
+    elements d + W t (global r M + d + W t, i.e. cyclic position r c2 + t of rank d); the received
+    chunks in source order ARE the cyclic slice (prover_dist.cpp block_to_cyc, dist.hip k_pack_b2c)"""
+    M = len(blocks[0])
+    c2 = M // W
+    send = [[blk[d + W * t] for d in range(W) for t in range(c2)] for blk in blocks]
+    return alltoall(send, W)
+
+
 # ------------------------------------------------------------------ tests
 @pytest.mark.parametrize("W,logN", [(2, 3), (2, 5), (4, 4), (4, 6), (8, 6)])
 def test_dft_roundtrip_matches_oracle(W, logN):
@@ -171,6 +181,15 @@ def test_cyclic_to_block(W, logL):
     L = 1 << logL
     x = [rnd.randrange(R) for _ in range(L)]
     assert cyclic_to_block(to_cyclic(x, W), W) == to_block(x, W)
+
+
+@pytest.mark.parametrize("W,logL", [(2, 3), (4, 5), (8, 7), (8, 8)])
+def test_block_to_cyclic(W, logL):
+    rnd = random.Random(100 + logL)
+    L = 1 << logL
+    x = [rnd.randrange(R) for _ in range(L)]
+    assert block_to_cyclic(to_block(x, W), W) == to_cyclic(x, W)
+    assert cyclic_to_block(block_to_cyclic(to_block(x, W), W), W) == to_block(x, W)
 
 
 def test_builder_scan_over_ranks():

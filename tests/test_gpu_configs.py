@@ -124,9 +124,73 @@ def test_c3_grandproduct_2p20(K):
     check_large(K, "grandproduct", 20, 1, False, 0xC3)
 
 
+_C4 = {}
+
+
+def c4_single(K):
+    """BASELINE configs[3] on one GPU (checked by check_large), shared by the 2^24 sharded tests"""
+    if "proof" not in _C4:
+        _C4["proof"] = check_large(K, "grandsum", 24, 1, False, 0xC4)
+    return _C4["proof"]
+
+
 def test_c4_grandsum_2p24(K):
     """BASELINE configs[3]: grand-sum n = 2^24, k = 1, one GPU."""
-    check_large(K, "grandsum", 24, 1, False, 0xC4)
+    c4_single(K)
+
+
+def test_c4_msm_sharded_2p24_w8(K):
+    """configs[3]'s MSM point-range split at its own size: n = 2^24 over 8 simulated ranks on cuda:0
+    (polynomial.js:1106-1115 split by point range); every rank == the one-GPU proof, byte for byte"""
+    want = c4_single(K)
+    nbits = 24
+    path = gpu_ptau(K, nbits)
+    Fs, Ts, sF, sT = np_inputs(0xC4, nbits, 1, False)
+    got = _sharded(K, 8, path, nbits, K.GRANDSUM, Fs, Ts, sF, sT)
+    cn, en = K.proof_names(K.GRANDSUM, 1, False)
+    for r in range(8):
+        assert got[r] == ([want["commitments"][c] for c in cn], [want["evaluations"][e] for e in en]), r
+
+
+def test_c4_distributed_2p24_w8_sliced(K):
+    """configs[3] through the distributed prover at its own size: n = 2^24, W = 8 simulated ranks on
+    cuda:0 (in-process group), every vector sharded and every rank holding ONLY its SRS slice (1/8 of
+    the window tables); all ranks' proofs == the one-GPU proof, byte for byte (hence verified)"""
+    want = c4_single(K)
+    nbits, world = 24, 8
+    path = gpu_ptau(K, nbits)
+    Fs, Ts, sF, sT = np_inputs(0xC4, nbits, 1, False)
+    full = K.Context(0)
+    full.load_ptau(path, nbits)
+    full_bytes = full.srs_slice_info()[2]
+    full.close()
+    g = K.Group.local(world)
+    ctxs = [K.Context(0) for _ in range(world)]
+    for r, c in enumerate(ctxs):
+        c.load_ptau(path, nbits, slice=(r, world))
+        assert c.srs_slice_info()[2] * world == full_bytes
+    out, err = [None] * world, [None] * world
+
+    def run(r):
+        try:
+            out[r] = ctxs[r].prove(K.GRANDSUM, nbits, Fs, Ts, sF, sT, mont_out=False)[:2]
+        except Exception as e:  # pragma: no cover
+            err[r] = e
+    for r, c in enumerate(ctxs):
+        c.set_group(g, r)
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    for c in ctxs:
+        c.set_group(None)
+        c.close()
+    g.close()
+    assert not any(err), err
+    cn, en = K.proof_names(K.GRANDSUM, 1, False)
+    for r in range(world):
+        assert out[r] == ([want["commitments"][c] for c in cn], [want["evaluations"][e] for e in en]), r
 
 
 def test_c5_selected_vector_2p22_k4(K):

@@ -31,10 +31,16 @@ def single(K, ptau, kind, nbits, Fs, Ts, sF, sT):
     return out
 
 
-def run_group(K, group, world, ptau, kind, nbits, Fs, Ts, sF, sT, mont_out=False):
-    ctxs = [K.Context(0) for _ in range(world)]
+def run_group(K, group, world, ptau, kind, nbits, Fs, Ts, sF, sT, mont_out=False, sliced=False, ctxs=None,
+              keep=False):
+    """one proof over `world` contexts on cuda:0 (one host thread per rank); sliced: every rank
+    loads only its SRS slice (kgs_srs_load_ptau_slice), otherwise the whole SRS"""
+    own = ctxs is None
+    if own:
+        ctxs = [K.Context(0) for _ in range(world)]
+        for r, c in enumerate(ctxs):
+            c.load_ptau(ptau, nbits, slice=(r, world) if sliced else None)
     for r, c in enumerate(ctxs):
-        c.load_ptau(ptau, nbits)
         c.set_group(group, r)
     out, err = [None] * world, [None] * world
 
@@ -51,7 +57,8 @@ def run_group(K, group, world, ptau, kind, nbits, Fs, Ts, sF, sT, mont_out=False
         t.join(timeout=600)
     for c in ctxs:
         c.set_group(None)
-        c.close()
+        if own and not keep:
+            c.close()
     return out, err
 
 
@@ -73,6 +80,73 @@ def test_local_group_equals_single_gpu(K, world, kind, nbits, npols, sel):
     assert not any(err), err
     for r in range(world):
         assert got[r] == want, r
+
+
+SLICED = [(2, 0, 5, 1, False), (4, 1, 9, 2, True), (8, 0, 11, 3, True), (8, 1, 12, 1, False), (4, 0, 16, 1, False)]
+
+
+@pytest.mark.parametrize("world,kind,nbits,npols,sel", SLICED)
+def test_sliced_srs_group_equals_single_gpu(K, world, kind, nbits, npols, sel):
+    """every rank holds only its SRS slice (points r + W j): the proof is still byte-identical"""
+    ptau = gpu_ptau(K, max(nbits, 9))
+    Fs, Ts, sF, sT = common.make_inputs(7000 + 31 * world + nbits + npols, nbits, npols, sel)
+    want = single(K, ptau, kind, nbits, Fs, Ts, sF, sT)
+    g = K.Group.local(world)
+    got, err = run_group(K, g, world, ptau, kind, nbits, Fs, Ts, sF, sT, sliced=True)
+    g.close()
+    assert not any(err), err
+    for r in range(world):
+        assert got[r] == want, r
+
+
+def test_slice_holds_one_wth_of_the_tables(K):
+    """kgs_srs_slice_info: a rank's slice is 1/W of the points (and, at the same window, of the bytes);
+    a context holding a slice refuses the single-GPU prover"""
+    nbits, world = 16, 8
+    ptau = gpu_ptau(K, nbits)
+    full = K.Context(0)
+    full.load_ptau(ptau, nbits)
+    _, npts_full, c_full = full.srs_info()
+    assert full.srs_slice_info()[:2] == (0, 1)
+    full.close()
+    for r in (0, 5):
+        c = K.Context(0)
+        c.load_ptau(ptau, nbits, slice=(r, world))
+        _, npts, cw = c.srs_info()
+        rank, w, tbytes = c.srs_slice_info()
+        assert (rank, w) == (r, world) and npts == npts_full // world
+        W = (255 + cw - 1) // cw
+        assert tbytes == W * npts * 64
+        Fs, Ts, sF, sT = common.make_inputs(5, 6, 1, False)
+        with pytest.raises(K.KgsError, match="SRS slice"):
+            c.prove(K.GRANDSUM, 6, Fs, Ts, sF, sT, mont_out=False)
+        c.close()
+
+
+def test_rank_local_failure_is_agreed(K):
+    """a precondition that fails on ONE rank (no SRS / another rank's slice) fails every rank at once
+    with that rank's error, before any exchange; the group stays usable"""
+    world, nbits = 4, 9
+    ptau = gpu_ptau(K, 9)
+    Fs, Ts, sF, sT = common.make_inputs(99, nbits, 1, False)
+    want = single(K, ptau, K.GRANDSUM, nbits, Fs, Ts, sF, sT)
+    g = K.Group.local(world)
+    ctxs = [K.Context(0) for _ in range(world)]
+    for r, c in enumerate(ctxs):
+        if r != 2:
+            c.load_ptau(ptau, nbits, slice=(r, world))
+    _, err = run_group(K, g, world, ptau, K.GRANDSUM, nbits, Fs, Ts, sF, sT, ctxs=ctxs)
+    assert all(isinstance(e, K.KgsError) and "no SRS loaded" in str(e) for e in err), err
+    ctxs[2].load_ptau(ptau, nbits, slice=(1, world))  # the wrong slice
+    _, err = run_group(K, g, world, ptau, K.GRANDSUM, nbits, Fs, Ts, sF, sT, ctxs=ctxs)
+    assert all(isinstance(e, K.KgsError) and "is not this context's" in str(e) for e in err), err
+    ctxs[2].load_ptau(ptau, nbits, slice=(2, world))
+    got, err = run_group(K, g, world, ptau, K.GRANDSUM, nbits, Fs, Ts, sF, sT, ctxs=ctxs)
+    assert not any(err), err
+    assert all(x == want for x in got)
+    for c in ctxs:
+        c.close()
+    g.close()
 
 
 @pytest.mark.parametrize("world,nbits,npols,sel", [(8, 20, 1, False), (4, 22, 2, True)])
