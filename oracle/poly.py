@@ -228,6 +228,30 @@ class Polynomial:
         self.coef = q
         return self
 
+    # polynomial.js:84-95 (equal up to each one's degree)
+    def is_equal(self, other):
+        d = self.degree()
+        if d != other.degree():
+            return False
+        return all(self.coef[i] % R == other.coef[i] % R for i in range(d + 1))
+
+    # polynomial.js:617-646: self <- quotient by (X^n - beta), returns the remainder polynomial (the
+    # dividend's buffer with the reduced coefficients); same length as the dividend
+    def div_by_vanishing(self, n, beta):
+        if self.degree() < n:
+            raise ValueError("divByVanishing polynomial divisor must be of degree lower than the dividend polynomial")
+        rem = list(self.coef)
+        q = [0] * self.length()
+        for i in range(self.length() - 1, n - 1, -1):
+            lead = rem[i] % R
+            if lead == 0:
+                continue
+            rem[i] = 0
+            rem[i - n] = (rem[i - n] + beta * lead) % R
+            q[i - n] = (q[i - n] + lead) % R
+        self.coef = q
+        return Polynomial(rem)
+
     # polynomial.js:853-888
     def div_zh(self, domain_size):
         n = domain_size

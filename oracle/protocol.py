@@ -422,7 +422,7 @@ def prove(kind, srs, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, trace=Non
     }
 
 
-def verify(kind, ptau, proof, nbits, tau=None):
+def verify(kind, ptau, proof, nbits, tau=None, trace=None):
     """src/grandsum/mset_eq_kzg_verifier.js:9-313 / src/grandproduct/mset_eq_kzg_verifier.js:9-299.
 
     With `tau` given, the final pairing check e(-A,[tau]_2)·e(B,[1]_2) == 1 is decided by the
@@ -565,6 +565,8 @@ def verify(kind, ptau, proof, nbits, tau=None):
     else:
         Bp = A(M(com["Wxi"], xi), M(com["Wxiw"], u * xi % R * w % R))
     Bp = A(A(Bp, F1), neg(E1p))
+    if trace is not None:  # the values the reference's verifier logs (verifier.js:73-74,99,122,143,167)
+        trace.update(challenges=dict(ch), zh=zh, l1=l1, r0=r0, D1=D1, F1=F1, E1=E1p)
     if tau is not None:
         return M(Ap, tau) == Bp
     return bn.pairing_eq(neg(Ap), ptau.tau_g2(), Bp, bn.G2_GEN)

@@ -59,6 +59,52 @@ def test_div_by_x_sub_value():
     assert p.coef == [4, (-3) % R, 7, 0]
 
 
+def test_polynomial_degree_kat():
+    # test/polynomial.test.js:31-70 (the degree sets the MSM length N of multiExponentiation,
+    # polynomial.js:1106-1115, and the Horner start of evaluate)
+    rnd = [7, 11, 13]
+    assert OP.Polynomial([]).degree() == 0          # no coefficients
+    assert OP.Polynomial([rnd[0]]).degree() == 0    # one coefficient
+    assert OP.Polynomial([rnd[0], rnd[1]]).degree() == 1
+    assert OP.Polynomial([rnd[0], 0]).degree() == 0  # the greatest is zero
+    buff = [rnd[0], 0, 0]
+    assert OP.Polynomial(buff).degree() == 0        # the two greatest are zero
+    buff[2] = 1
+    assert OP.Polynomial(buff).degree() == 2
+    # degree-based equality (polynomial.js:84-95): trailing zeros do not matter
+    assert OP.Polynomial([1, 2, 0, 0]).is_equal(OP.Polynomial([1, 2]))
+    assert not OP.Polynomial([1, 2, 3]).is_equal(OP.Polynomial([1, 2]))
+
+
+def test_div_by_vanishing_kat():
+    # test/polynomial.test.js:240-253: divByVanishing(2, 2) of the 19-coefficient dividend
+    e = lambda v: v % R  # noqa: E731  (Fr.e)
+    dividend = OP.Polynomial([e(v) for v in (-14, -2, 3, -5, -6, -7, -8, -9, -10, -11, -12, -13, -14, -15, -16, -17,
+                                             -18, 15, 16)])
+    quotient = OP.Polynomial([e(v) for v in (7, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16)])
+    rem = dividend.div_by_vanishing(2, e(2))
+    assert dividend.is_equal(quotient)
+    # and the identity dividend = q (X^2 - 2) + rem, with deg rem < 2
+    assert rem.degree() < 2
+    q = quotient.coef
+    recon = [0] * 19
+    for i, c in enumerate(q):
+        recon[i + 2] = (recon[i + 2] + c) % R
+        recon[i] = (recon[i] - 2 * c) % R
+    recon[0] = (recon[0] + rem.coef[0]) % R
+    recon[1] = (recon[1] + rem.coef[1]) % R
+    assert recon == [e(v) for v in (-14, -2, 3, -5, -6, -7, -8, -9, -10, -11, -12, -13, -14, -15, -16, -17, -18, 15, 16)]
+    # divZh is this division at beta = 1 (polynomial.js:853-888 specialises it): same quotient
+    p = OP.Polynomial([e(v) for v in (-1, 0, 0, 0, 1, 0, 0, 0)])  # X^4 - 1 = 1 * (X^4 - 1)
+    p.div_by_vanishing(4, 1)
+    assert p.is_equal(OP.Polynomial([1]))
+    try:
+        OP.Polynomial([1, 2]).div_by_vanishing(2, 1)
+        assert False, "a divisor of higher degree must throw"
+    except ValueError as err:
+        assert "must be of degree lower" in str(err)
+
+
 def test_ntt_roundtrip_and_definition():
     vals = [(i * 7919 + 3) % R for i in range(16)]
     ev = OP.ntt(vals, False)
