@@ -4,7 +4,8 @@
 // would be (src/grandsum/mset_eq_kzg_prover.js:12 is an independent async function per call).
 const fs = require("fs");
 const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_grandproduct_prover,
-        lookup_kzg_grandsum_prover } = require("../index");
+        lookup_kzg_grandsum_prover, mset_eq_kzg_grandsum_verifier, mset_eq_kzg_grandproduct_verifier,
+        lookup_kzg_grandsum_verifier } = require("../index");
 
 (async () => {
     const spec = JSON.parse(fs.readFileSync(process.argv[2], "utf8"));
@@ -21,6 +22,11 @@ const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_
             const o = { commitments: {}, evaluations: {}, montF: F.map(e => hex(e.eval)) };
             for (const k of Object.keys(proof.commitments)) o.commitments[k] = hex(proof.commitments[k]);
             for (const k of Object.keys(proof.evaluations)) o.evaluations[k] = hex(proof.evaluations[k]);
+            if (spec.verify) {  // the drop-in verifier of the same argument, as the reference's tests do
+                const vf = { grandsum: mset_eq_kzg_grandsum_verifier, grandproduct: mset_eq_kzg_grandproduct_verifier,
+                             lookup: lookup_kzg_grandsum_verifier }[c.kind];
+                o.verified = await vf(spec.ptau, proof, Math.log2(F[0].length()));
+            }
             return o;
         } catch (e) {
             return { error: e.message };

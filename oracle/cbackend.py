@@ -80,9 +80,11 @@ def msm(srs_bytes, scalars_mont, threads=0):
     return out.raw
 
 
-def cpu_baseline(nbits, kind="grandsum", threads=0, ptau=None, max_seconds=60.0):
-    """Time the C port on the bench workload (same generator as bench.py) — 1 proof (a 2nd if the
-    first took < 10 s). Returns the bench.py `cpu_baseline` object."""
+def cpu_baseline(nbits, kind="grandsum", threads=0, ptau=None, max_seconds=90.0, reps=3):
+    """Time the C port on the bench workload (same generator as bench.py) as BASELINE.md:84-87
+    prescribes: 1 warm-up proof, then the median of `reps` (>= 3) timed proofs, with their spread.
+    If the warm-up alone shows that warm-up + reps would exceed `max_seconds`, fewer timed proofs are
+    run (at least one) and the sample says so. Returns the bench.py `cpu_baseline` object."""
     import numpy as np
     n = 1 << nbits
     rng = np.random.Generator(np.random.PCG64(0x4B5A4753))
@@ -94,15 +96,19 @@ def cpu_baseline(nbits, kind="grandsum", threads=0, ptau=None, max_seconds=60.0)
     kk = 0 if kind == "grandsum" else 1
     if threads <= 0:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    times = []
-    while True:
+    fb, tb = [f.tobytes()], [t.tobytes()]
+
+    def one():
         t0 = time.perf_counter()
-        prove_raw(kk, nbits, [f.tobytes()], [t.tobytes()], None, None, srs, threads)
-        times.append(time.perf_counter() - t0)
-        if sum(times) > 10.0 or len(times) >= 3 or sum(times) > max_seconds:
-            break
-    per = min(times)
-    return {"value": round(1.0 / per, 5), "unit": "proofs/s", "cores": threads, "kind": "port",
-            "sample": f"{len(times)} full {kind} proof(s) at n=2^{nbits}, k=1 (oracle/c C restatement of the "
-                      f"reference op list incl. 4n multiply, OpenMP {threads} threads); best of {len(times)}: "
-                      f"{per:.2f} s/proof"}
+        prove_raw(kk, nbits, fb, tb, None, None, srs, threads)
+        return time.perf_counter() - t0
+    warm = one()
+    k = max(1, min(reps, int((max_seconds - warm) // max(warm, 1e-9))))
+    times = sorted(one() for _ in range(k))
+    med = times[len(times) // 2] if len(times) % 2 else 0.5 * (times[len(times) // 2 - 1] + times[len(times) // 2])
+    return {"value": round(1.0 / med, 5), "unit": "proofs/s", "cores": threads, "kind": "port",
+            "median_s_per_proof": round(med, 3), "min_s": round(times[0], 3), "max_s": round(times[-1], 3),
+            "spread_pct": round(100.0 * (times[-1] - times[0]) / med, 1), "warmup_s": round(warm, 3),
+            "sample": f"1 warm-up + median of {k} full {kind} proof(s) at n=2^{nbits}, k=1 (oracle/c C restatement "
+                      f"of the reference op list incl. 4n multiply, OpenMP {threads} threads): {med:.2f} s/proof "
+                      f"(min {times[0]:.2f}, max {times[-1]:.2f})" + ("" if k >= 3 else f"; capped at {max_seconds:.0f} s")}

@@ -74,6 +74,47 @@ def test_js_proofs_match_oracle(tmp_path):
 
 
 @pytest.mark.gpu
+def test_js_reference_ranges_c1(tmp_path):
+    """The reference's own test ranges through the JS drop-in (test/mset_eq_kzg_grandsum.test.js:24-104
+    and the grand-product twin: nBits = getRandomValue(1, 10), nPols = getRandomValue(2, 10), the four
+    variants, T = F rotated by one, selectors ones but the last / the first) on a power-11 ptau, plus
+    every variant at C1's nBits = 11 (BASELINE configs[0]): each proof byte-exact vs the C oracle's and
+    accepted by the drop-in verifier of its argument."""
+    import random
+    from oracle import cbackend as C
+    ptau = common.oracle_ptau(11)
+    srs = C.load_srs_bytes(ptau)[1]
+    rnd = random.Random(0xC1)
+    get_random_value = lambda lo, hi: max(lo, rnd.randint(1, hi))  # noqa: E731  (test.utils.js:1-6)
+    cases, expect = [], []
+    seed = 11000
+    for kind in ("grandsum", "grandproduct"):
+        for vec, sel in ((False, False), (True, False), (False, True), (True, True)):
+            for nbits in (11, get_random_value(1, 10)):
+                npols = get_random_value(2, 10) if vec else 1
+                Fs, Ts, sF, sT = common.make_inputs(seed, nbits, npols, sel)
+                seed += 1
+                cases.append({"kind": kind, "F": [x.hex() for x in Fs], "T": [x.hex() for x in Ts],
+                              "selF": sF.hex() if sF else None, "selT": sT.hex() if sT else None})
+                coms, evs = C.prove_raw(0 if kind == "grandsum" else 1, nbits, Fs, Ts, sF, sT, srs)
+                expect.append((kind, nbits, npols, sel, coms, evs))
+    spec = tmp_path / "spec.json"
+    spec.write_text(json.dumps({"ptau": ptau, "cases": cases, "verify": True}))
+    out = json.loads(subprocess.check_output([NODE, os.path.join(JS, "test", "prove_from_json.js"), str(spec)],
+                                             timeout=900))
+    K = common.load_pkg()
+    assert len(out["proofs"]) == len(expect) == 16
+    assert sum(1 for e in expect if e[1] == 11) == 8
+    for got, (kind, nbits, npols, sel, coms, evs) in zip(out["proofs"], expect):
+        assert "error" not in got, got
+        kk = K.GRANDSUM if kind == "grandsum" else K.GRANDPRODUCT
+        cn, en = K.proof_names(kk, npols, sel)
+        assert [got["commitments"][c] for c in cn] == [x.hex() for x in coms], (kind, nbits, npols, sel)
+        assert [got["evaluations"][e] for e in en] == [x.hex() for x in evs], (kind, nbits, npols, sel)
+        assert got["verified"] is True, (kind, nbits, npols, sel)
+
+
+@pytest.mark.gpu
 def test_js_concurrent_provers_match_oracle(tmp_path):
     """12 prover() Promises in flight at once (Promise.all), grand-sum and grand-product mixed, 1-3
     vectors, with and without selectors, two domain sizes: every proof byte-identical to the oracle
