@@ -48,7 +48,7 @@ struct MsmWork {
   uint32_t *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *sorted = nullptr;
   uint32_t* part = nullptr;      // bucket row + column sums (2^h + 2^l run records, msm.hip k_rowcol)
   uint32_t* segowner = nullptr;  // bucket of each segment's first run
-  uint32_t* locnt = nullptr;     // lo pass: 256 partitions x 256 lo x 16 chunks counts / bases
+  uint32_t* locnt = nullptr;     // lo pass: 256 partitions x 256 lo x 64 chunks counts / bases
   uint32_t* chunklist = nullptr; // combine levels: 3 lists of chunk-start segments
   uint32_t* chunkcnt = nullptr;  // their lengths
   uint32_t* raw29 = nullptr;     // accumulate output in the fq29 form (B + 1 + nseg entries x 160 B)

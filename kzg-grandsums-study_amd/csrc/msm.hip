@@ -204,13 +204,22 @@ __global__ void __launch_bounds__(256) k_sort_scan_blocks(uint32_t* __restrict__
   if (threadIdx.x == 255) ptot[blockIdx.x] = part[255];
 }
 
-// hi_off[p] = exclusive scan of partition totals (NH <= 256); offsets[B+1] = total
+__device__ __forceinline__ uint32_t chunk_count(uint32_t size);
+
+// hi_off[p] = exclusive scan of partition totals (NH <= 256); offsets[B+1] = total; cpre = exclusive
+// scan of the lo pass's chunks per partition (cpre[NH] = all chunks)
 __global__ void __launch_bounds__(64) k_sort_scan(uint32_t* __restrict__ hi_off, const uint32_t* __restrict__ ptot,
-                                                  int NH, uint32_t* __restrict__ offsets, uint32_t B) {
+                                                  int NH, uint32_t* __restrict__ offsets, uint32_t B,
+                                                  uint32_t* __restrict__ cpre) {
   KGS_AUX_PRIO();
+  __shared__ uint32_t gp[256];
   const uint32_t total = wave_excl_scan256(ptot, hi_off, NH);
+  for (int q = threadIdx.x; q < NH; q += 64) gp[q] = chunk_count(ptot[q]);
+  __syncthreads();
+  const uint32_t chunks = wave_excl_scan256(gp, cpre, NH);
   if (threadIdx.x == 0) {
     hi_off[NH] = total;
+    cpre[NH] = chunks;
     offsets[0] = 0;  // key 0 (zero digits) is never stored
     offsets[B + 1] = total;
   }
@@ -272,33 +281,70 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
   }
 }
 
-// Pass 2: every partition p is cut into SL_G chunks; (1) per-chunk LDS histograms of lo, (2) one
+// Pass 2: every partition p is cut into G_p chunks; (1) per-chunk LDS histograms of lo, (2) one
 // workgroup per partition scans them into per-(lo, chunk) global bases and writes the bucket
-// offsets, (3) every chunk counting-sorts its entries tile by tile through LDS and writes runs.
-// Chunks keep a skewed partition (all points in one bucket: a selector polynomial's equal
-// coefficients) spread over SL_G workgroups instead of one.
+// offsets, (3) every chunk counting-sorts its entries through LDS and writes runs.
+// G_p = clamp(ceil(size_p / SL_CHUNK), 1, SL_G): a chunk of a uniform partition fits ONE LDS tile,
+// so each of its buckets leaves as one run of ~SL_CHUNK / 256 entries (≈ 190 B at 2^20 points: whole
+// 128-byte lines, where the round-2 tiles of a 16-way split wrote ≈ 60-byte runs, 1.46× write
+// amplification); a skewed partition (all points in one bucket: a selector polynomial's equal
+// coefficients) is spread over up to SL_G workgroups. -DKGS_SL_FIXED16 restores the fixed 16-way
+// split with 4096-entry tiles (A/B).
 constexpr int SL_THREADS = 1024;
-#ifndef KGS_SL_TILE
-#define KGS_SL_TILE 4096
-#endif
-constexpr int SL_TILE = KGS_SL_TILE;
+#ifdef KGS_SL_FIXED16
+constexpr int SL_TILE = 4096;
 constexpr int SL_G = 16;
+constexpr uint32_t SL_CHUNK = 0;  // unused: always SL_G chunks
+#else
+constexpr int SL_TILE = 12288;
+constexpr int SL_G = 64;
+constexpr uint32_t SL_CHUNK = 12288;
+#endif
 
-__device__ __forceinline__ void chunk_range(uint32_t s0, uint32_t s1, int g, uint32_t& c0, uint32_t& c1) {
-  const uint32_t csz = (s1 - s0 + SL_G - 1) / SL_G;
+// chunks of a partition of `size` entries
+__device__ __forceinline__ uint32_t chunk_count(uint32_t size) {
+  if (SL_CHUNK == 0) return SL_G;
+  const uint32_t g = (size + SL_CHUNK - 1) / SL_CHUNK;
+  return g < 1 ? 1u : g > (uint32_t)SL_G ? (uint32_t)SL_G : g;
+}
+
+// The lo-pass kernels run one workgroup per (partition, chunk) on a 1-D grid: cpre[p] = chunks of
+// the partitions before p (k_sort_scan), block b belongs to the partition p with
+// cpre[p] <= b < cpre[p + 1]; blocks past cpre[NH] (the host sizes the grid by an upper bound) exit.
+__device__ __forceinline__ bool chunk_of_block(const uint32_t* cpre, int NH, uint32_t b, uint32_t& p, uint32_t& g,
+                                               uint32_t& G) {
+  if (b >= cpre[NH]) return false;
+  uint32_t lo = 0, hi = (uint32_t)NH;  // cpre[lo] <= b < cpre[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (cpre[mid] <= b) lo = mid; else hi = mid;
+  }
+  p = lo;
+  g = b - cpre[lo];
+  G = cpre[lo + 1] - cpre[lo];
+  return true;
+}
+
+__device__ __forceinline__ void chunk_range(uint32_t s0, uint32_t s1, uint32_t G, uint32_t g, uint32_t& c0,
+                                            uint32_t& c1) {
+  const uint32_t csz = (s1 - s0 + G - 1) / G;
   c0 = s0 + g * csz < s1 ? s0 + g * csz : s1;
   c1 = c0 + csz < s1 ? c0 + csz : s1;
 }
 
-// grid (SL_G, NH): locnt[(p * nb + lo) * SL_G + g] = #entries of chunk g of partition p with this lo
+// one block per (partition, chunk): locnt[(p * nb + lo) * SL_G + g] = #entries of chunk g of
+// partition p with this lo
 __global__ void __launch_bounds__(SL_THREADS) k_lo_count(uint32_t* __restrict__ locnt, const uint8_t* __restrict__ tlo,
-                                                         const uint32_t* __restrict__ hi_off, int lob) {
+                                                         const uint32_t* __restrict__ hi_off,
+                                                         const uint32_t* __restrict__ cpre, int NH, int lob) {
   KGS_AUX_PRIO();
   __shared__ uint32_t cnt[256];
-  const int g = blockIdx.x, p = blockIdx.y;
+  uint32_t p, g, G;
+  if (!chunk_of_block(cpre, NH, blockIdx.x, p, g, G)) return;  // uniform per block
   const int nb = 1 << lob;
+  const uint32_t s0 = hi_off[p], s1 = hi_off[p + 1];
   uint32_t c0, c1;
-  chunk_range(hi_off[p], hi_off[p + 1], g, c0, c1);
+  chunk_range(s0, s1, G, g, c0, c1);
   if ((int)threadIdx.x < nb) cnt[threadIdx.x] = 0;
   __syncthreads();
   for (uint32_t e = c0 + threadIdx.x; e < c1; e += SL_THREADS) atomicAdd(&cnt[tlo[e]], 1u);
@@ -308,16 +354,18 @@ __global__ void __launch_bounds__(SL_THREADS) k_lo_count(uint32_t* __restrict__ 
 
 // grid NH, 256 threads: bases (in place over locnt) and the bucket offsets of keys (p << lob) + lo + 1
 __global__ void __launch_bounds__(256) k_lo_scan(uint32_t* __restrict__ locnt, uint32_t* __restrict__ offsets,
-                                                 const uint32_t* __restrict__ hi_off, int lob) {
+                                                 const uint32_t* __restrict__ hi_off,
+                                                 const uint32_t* __restrict__ cpre, int lob) {
   KGS_AUX_PRIO();
   __shared__ uint32_t tot[256], pre[256];
   const int p = blockIdx.x;
   const int nb = 1 << lob;
+  const uint32_t G = cpre[p + 1] - cpre[p];
   const uint32_t lo = threadIdx.x;
   uint32_t* row = locnt + ((uint64_t)p * nb + lo) * SL_G;
   uint32_t run = 0;
   if ((int)lo < nb)
-    for (int g = 0; g < SL_G; g++) {
+    for (uint32_t g = 0; g < G; g++) {
       const uint32_t v = row[g];
       row[g] = run;
       run += v;
@@ -329,25 +377,28 @@ __global__ void __launch_bounds__(256) k_lo_scan(uint32_t* __restrict__ locnt, u
   if ((int)lo < nb) {
     const uint32_t base = hi_off[p] + pre[lo];
     offsets[((uint32_t)p << lob) + lo + 1] = base;
-    for (int g = 0; g < SL_G; g++) row[g] += base;
+    for (uint32_t g = 0; g < G; g++) row[g] += base;
   }
 }
 
-// grid (SL_G, NH): chunk g of partition p, tiles of SL_TILE through LDS, run-wise stores
+// one block per (partition, chunk): chunk g of partition p, tiles of SL_TILE through LDS, run-wise stores
 __global__ void __launch_bounds__(SL_THREADS) k_lo_scatter(uint32_t* __restrict__ sorted,
                                                            const uint32_t* __restrict__ locnt,
                                                            const uint32_t* __restrict__ tval,
                                                            const uint8_t* __restrict__ tlo,
-                                                           const uint32_t* __restrict__ hi_off, int lob) {
+                                                           const uint32_t* __restrict__ hi_off,
+                                                           const uint32_t* __restrict__ cpre, int NH, int lob) {
   KGS_AUX_PRIO();
   __shared__ uint32_t cur[256], tcnt[256], toff[256];
   __shared__ uint32_t sv[SL_TILE];
   __shared__ uint8_t sl[SL_TILE];
-  const int g = blockIdx.x, p = blockIdx.y;
+  uint32_t p, g, G;
+  if (!chunk_of_block(cpre, NH, blockIdx.x, p, g, G)) return;  // uniform per block
   const uint32_t tid = threadIdx.x;
   const int nb = 1 << lob;
+  const uint32_t s0 = hi_off[p], s1 = hi_off[p + 1];
   uint32_t c0, c1;
-  chunk_range(hi_off[p], hi_off[p + 1], g, c0, c1);
+  chunk_range(s0, s1, G, g, c0, c1);
   if (c0 >= c1) return;  // uniform per block
   if ((int)tid < nb) cur[tid] = locnt[((uint64_t)p * nb + tid) * SL_G + g];
   __syncthreads();
@@ -683,6 +734,7 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   const uint32_t nblk = (uint32_t)((N + 256 * SORT_SPT - 1) / (256 * SORT_SPT));
   uint32_t* ptot = w.counts;           // NH partition totals
   uint32_t* hi_off = w.cursor;         // NH + 1
+  uint32_t* cpre = w.cursor + 300;     // NH + 1: lo-pass chunks per partition, exclusive scan
   uint32_t* bh = w.blockhist;          // NH x nblk
   const size_t part_lds = (size_t)256 * SORT_SPT * W * 6;
   switch (c) {
@@ -690,7 +742,7 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   case CC:                                                                                                      \
     hipLaunchKernelGGL(k_sort_hist<CC>, dim3(nblk), dim3(256), 0, st, bh, scalars, N, lob, NH, nblk);         \
     hipLaunchKernelGGL(k_sort_scan_blocks, dim3(NH), dim3(256), 0, st, bh, ptot, nblk);                       \
-    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(64), 0, st, hi_off, ptot, NH, w.offsets, B);               \
+    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(64), 0, st, hi_off, ptot, NH, w.offsets, B, cpre);         \
     hipLaunchKernelGGL(k_sort_part<CC>, dim3(nblk), dim3(256), part_lds, st, (uint32_t*)w.digit, w.lo, bh,   \
                        ptot, hi_off, scalars, N, tb.npts, pbase, pstride, lob, NH, nblk);                     \
     break;
@@ -700,10 +752,14 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
     default:
       return;  // choose_c keeps 7 <= c <= 17
   }
-  hipLaunchKernelGGL(k_lo_count, dim3(SL_G, NH), dim3(SL_THREADS), 0, st, w.locnt, w.lo, hi_off, lob);
-  hipLaunchKernelGGL(k_lo_scan, dim3(NH), dim3(256), 0, st, w.locnt, w.offsets, hi_off, lob);
-  hipLaunchKernelGGL(k_lo_scatter, dim3(SL_G, NH), dim3(SL_THREADS), 0, st, w.sorted, w.locnt,
-                     (const uint32_t*)w.digit, w.lo, hi_off, lob);
+  // lo-pass grid: an upper bound of sum_p chunk_count(size_p) (blocks past cpre[NH] exit)
+  const uint64_t chunk_bound = SL_CHUNK ? std::min<uint64_t>((uint64_t)NH * SL_G, NH + N * (uint64_t)W / SL_CHUNK)
+                                        : (uint64_t)NH * SL_G;
+  hipLaunchKernelGGL(k_lo_count, dim3((unsigned)chunk_bound), dim3(SL_THREADS), 0, st, w.locnt, w.lo, hi_off, cpre, NH,
+                     lob);
+  hipLaunchKernelGGL(k_lo_scan, dim3(NH), dim3(256), 0, st, w.locnt, w.offsets, hi_off, cpre, lob);
+  hipLaunchKernelGGL(k_lo_scatter, dim3((unsigned)chunk_bound), dim3(SL_THREADS), 0, st, w.sorted, w.locnt,
+                     (const uint32_t*)w.digit, w.lo, hi_off, cpre, NH, lob);
   if (ev) hipEventRecord(ev[1], st);
   const uint64_t E = N * (uint64_t)W;  // upper bound of nonzero entries
   // one segment per resident thread (KGS_ACC_WAVES blocks of 256 per CU): every accumulate

@@ -198,7 +198,7 @@ void ensure_msm_work(kgs_ctx& c) {
     w.offsets = c.buf("msm_offsets" + sfx, 4 * (B + 4));
     w.cursor = c.buf("msm_cursor" + sfx, 4 * (B + 600));
     w.segowner = c.buf("msm_segowner" + sfx, 4 * nseg);
-    w.locnt = c.buf("msm_locnt" + sfx, 4 * 256 * 256 * 16);
+    w.locnt = c.buf("msm_locnt" + sfx, 4 * 256 * 256 * 64);  // partitions x lo x chunks (msm.hip SL_G)
     w.chunklist = c.buf("msm_chunklist" + sfx, 4 * 3 * (nseg / 16 + B + 16));
     w.chunkcnt = c.buf("msm_chunkcnt" + sfx, 64);
     w.raw29 = c.buf("msm_raw29" + sfx, 160 * ((size_t)B + 2 + nseg));

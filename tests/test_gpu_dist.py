@@ -114,7 +114,7 @@ def test_slice_holds_one_wth_of_the_tables(K):
         c.load_ptau(ptau, nbits, slice=(r, world))
         _, npts, cw = c.srs_info()
         rank, w, tbytes = c.srs_slice_info()
-        assert (rank, w) == (r, world) and npts == npts_full // world
+        assert (rank, w) == (r, world) and npts == (npts_full - r + world - 1) // world  # points r + W j
         W = (255 + cw - 1) // cw
         assert tbytes == W * npts * 64
         Fs, Ts, sF, sT = common.make_inputs(5, 6, 1, False)
