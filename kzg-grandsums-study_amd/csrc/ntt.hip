@@ -176,12 +176,14 @@ static inline unsigned nblocks(uint64_t work, unsigned bs = 256) { return (unsig
 // log2 LB) or 2^(logd+K) (otherwise) elements, loaded and stored in address order (coalesced).
 // LDS layout: element e = j * LB + (col - b*LB) as two 16-byte halves in two planes, lo[e] and hi[e]:
 // the lanes of a wave touch consecutive 16-byte slots, so every ds_read_b128 / ds_write_b128 is
-// bank-conflict free (a 32-byte element stride put two lanes of each 16-lane group on the same banks:
-// 2-way conflicts, MI355X_MICROARCH.md LDS table). Tile size: 2^10 elements (32 KiB) lets five blocks
-// share a CU's 160 KiB, so the pass runs at its register-limited occupancy instead of the two blocks
-// per CU a 64 KiB tile allows.
+// bank-conflict free in the DIF passes (a 32-byte element stride put two lanes of each 16-lane group on
+// the same banks: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.50 -> 0.04; profiles/r03/ntt_counters.txt).
+// 2^21 pair 0.625 -> 0.616 ms (same-box A/B, profiles/r03/ntt_ab.txt): LDS was never the limiter —
+// the pass waves sit 37-41 % of their cycles parked on global loads and barriers at 2 blocks (8 waves)
+// per CU. Tile size: 2^11 elements (64 KiB, 256 threads); 2^10-element tiles with 128 threads
+// (-DKGS_NTT_ELOG=10: five blocks per CU) measured 16 % slower.
 #ifndef KGS_NTT_ELOG
-#define KGS_NTT_ELOG 10
+#define KGS_NTT_ELOG 11
 #endif
 constexpr int NTT_ELOG = KGS_NTT_ELOG;
 constexpr int LDS_ELEMS = 1 << NTT_ELOG;
