@@ -175,7 +175,7 @@ struct kgs_ctx {
   // bucket accumulation
   hipStream_t st2 = nullptr;
   hipStream_t st_copy = nullptr;  // Montgomery write-back of the host-buffer boundary
-  hipEvent_t ev_fork = nullptr, ev_copy = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_copy = nullptr, ev_copy2 = nullptr;
   std::vector<hipEvent_t> ev_in;  // kgs_prove: one per input vector DMA'd on the copy stream
   MsmWork mw2;
   int msm_lanes = 2;  // kgs_ctx_set_msm_lanes
@@ -207,6 +207,7 @@ struct kgs_ctx {
     if (h_io) hipHostFree(h_io);
     if (ev_fork) hipEventDestroy(ev_fork);
     if (ev_copy) hipEventDestroy(ev_copy);
+    if (ev_copy2) hipEventDestroy(ev_copy2);
     for (hipEvent_t e : ev_in) hipEventDestroy(e);
     if (st_copy) hipStreamDestroy(st_copy);
     if (st2) hipStreamDestroy(st2);
@@ -314,7 +315,7 @@ namespace kgsi {
 // ------------------------------------------------------------------ building blocks (prover.cpp)
 void ensure_domain(kgs_ctx& c, int logM);
 uint32_t* get_nxm1(kgs_ctx& c, int nbits, int lcs);
-void intt_nat(kgs_ctx& c, uint32_t* out, const uint32_t* in, int logm);
+void intt_nat(kgs_ctx& c, uint32_t* out, const uint32_t* in, int logm, hipStream_t st = nullptr);
 void coset_fwd(kgs_ctx& c, uint32_t* out, const uint32_t* in, uint64_t len, int lcs);
 void coset_inv(kgs_ctx& c, uint32_t* out, const uint32_t* in, int lcs);
 
@@ -380,6 +381,8 @@ struct ProveIn {
   // kgs_prove: per input vector (F_i at 2i, T_i at 2i + 1, then selF, selT) an event the main stream
   // waits for before the vector's first kernel, or nullptr (already ordered on the main stream)
   std::vector<hipEvent_t> ready;
+  // kgs_prove: blocks until vector v's DMA (and ready[v]) has been enqueued; null: all already are
+  std::function<void(size_t)> input_issued;
 };
 enum R5Poly { R5_S, R5_Q, R5_F, R5_T, R5_SELF, R5_SELT, R5_POLT };
 struct R5Term {

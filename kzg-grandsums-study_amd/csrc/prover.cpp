@@ -42,6 +42,7 @@
 #include "ptau_io.hpp"
 #include "transcript.hpp"
 
+#include <condition_variable>
 #include "context.hpp"
 
 using namespace kgs;
@@ -150,8 +151,8 @@ uint32_t* get_nxm1(kgs_ctx& c, int nbits, int lcs) {
 
 // ------------------------------------------------------------------ NTT helpers
 // natural-order evaluations -> natural-order coefficients (out != in)
-void intt_nat(kgs_ctx& c, uint32_t* out, const uint32_t* in, int logm) {
-  ntt_dit(c.st, out, in, 0, logm, c.tw_inv, c.logM, nullptr, c.invm + 8 * logm);
+void intt_nat(kgs_ctx& c, uint32_t* out, const uint32_t* in, int logm, hipStream_t st) {
+  ntt_dit(st ? st : c.st, out, in, 0, logm, c.tw_inv, c.logM, nullptr, c.invm + 8 * logm);
 }
 // coefficients (len <= 2^lcs, natural) -> coset evaluations p(g w^i), bit-reversed order
 void coset_fwd(kgs_ctx& c, uint32_t* out, const uint32_t* in, uint64_t len, int lcs) {
@@ -621,22 +622,55 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
 
   // ---------------- round 1: witness polynomials + commitments (prover.js:144-179)
   std::vector<uint32_t*> fm(k), tm(k), Fc(k), Tc(k);
-  auto wait_input = [&](size_t v) {  // pipelined host-buffer inputs (kgs_prove)
-    if (v < in.ready.size() && in.ready[v]) HC(hipStreamWaitEvent(c.st, in.ready[v], 0));
-  };
   for (int i = 0; i < k; i++) {
     fm[i] = c.buf("fm" + std::to_string(i), E);
     tm[i] = c.buf("tm" + std::to_string(i), E);
     Fc[i] = c.buf("Fc" + std::to_string(i), E);
     Tc[i] = c.buf("Tc" + std::to_string(i), E);
-    wait_input(2 * i);
-    launch_to_mont(c.st, fm[i], in.f_std[i], n);
-    wait_input(2 * i + 1);
-    launch_to_mont(c.st, tm[i], in.t_std[i], n);
-    intt_nat(c, Fc[i], fm[i], nbits);
-    intt_nat(c, Tc[i], tm[i], nbits);
   }
-  check_launch();
+  uint32_t *sFc = nullptr, *sTc = nullptr;
+  if (sel) {
+    sFc = c.buf("sFc", E);
+    sTc = c.buf("sTc", E);
+  }
+  // Host-buffer inputs (kgs_prove) arrive vector by vector: in.input_issued(v) returns once vector
+  // v's DMA is enqueued (its host copy may still be running on another thread before that), and
+  // in.ready[v] is the event its first kernel waits for.
+  auto wait_input = [&](size_t v, hipStream_t st) {
+    if (in.input_issued) in.input_issued(v);
+    if (v < in.ready.size() && in.ready[v]) HC(hipStreamWaitEvent(st, in.ready[v], 0));
+  };
+  std::vector<Commit> r1;
+  int slot = 0;
+  // With two MSM lanes (a proof alone on its context: the latency mode) each input vector's whole
+  // round-1 chain — Montgomery conversion, iNTT, commitment MSM — runs on the lane of its
+  // commitment, F_i / selF on lane 0 and T_i / selT on lane 1, so that T's transfer (host buffers)
+  // and T's transform overlap F's MSM instead of delaying it.
+  const bool piped = split_commits(c);
+  if (piped) {
+    fork_lanes(c);
+    for (int i = 0; i < k; i++) {
+      wait_input(2 * i, c.st);
+      launch_to_mont(c.st, fm[i], in.f_std[i], n);
+      intt_nat(c, Fc[i], fm[i], nbits);
+      r1.push_back(commit_launch(c, Fc[i], n, slot++, 0));
+      wait_input(2 * i + 1, c.st2);
+      launch_to_mont(c.st2, tm[i], in.t_std[i], n);
+      intt_nat(c, Tc[i], tm[i], nbits, c.st2);
+      r1.push_back(commit_launch(c, Tc[i], n, slot++, 1));
+    }
+    check_launch();
+  } else {
+    for (int i = 0; i < k; i++) {
+      wait_input(2 * i, c.st);
+      launch_to_mont(c.st, fm[i], in.f_std[i], n);
+      wait_input(2 * i + 1, c.st);
+      launch_to_mont(c.st, tm[i], in.t_std[i], n);
+      intt_nat(c, Fc[i], fm[i], nbits);
+      intt_nat(c, Tc[i], tm[i], nbits);
+    }
+    check_launch();
+  }
   // Montgomery write-back (prover.js:147-148) on the copy stream, overlapping round 1's MSMs;
   // fm/tm are not written again before the round-1 sync
   bool wb = false;
@@ -648,30 +682,41 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     }
     HC(hipEventRecord(c.ev_copy, c.st));
     HC(hipStreamWaitEvent(c.st_copy, c.ev_copy, 0));
+    if (piped) {  // the T_i conversions ran on lane 1
+      if (!c.ev_copy2) HC(hipEventCreateWithFlags(&c.ev_copy2, hipEventDisableTiming));
+      HC(hipEventRecord(c.ev_copy2, c.st2));
+      HC(hipStreamWaitEvent(c.st_copy, c.ev_copy2, 0));
+    }
     for (int i = 0; i < k; i++) {
       if (in.mont_f_out[i]) HC(hipMemcpyAsync(in.mont_f_out[i], fm[i], E, hipMemcpyDeviceToHost, c.st_copy));
       if (in.mont_t_out[i]) HC(hipMemcpyAsync(in.mont_t_out[i], tm[i], E, hipMemcpyDeviceToHost, c.st_copy));
     }
   }
-  uint32_t *sFc = nullptr, *sTc = nullptr;
   if (sel) {
-    sFc = c.buf("sFc", E);
-    sTc = c.buf("sTc", E);
-    wait_input(2 * k);
-    intt_nat(c, sFc, in.sel_f, nbits);
-    wait_input(2 * k + 1);
-    intt_nat(c, sTc, in.sel_t, nbits);
+    if (piped) {
+      wait_input(2 * k, c.st);
+      intt_nat(c, sFc, in.sel_f, nbits);
+      r1.push_back(commit_launch(c, sFc, n, slot++, 0));
+      wait_input(2 * k + 1, c.st2);
+      intt_nat(c, sTc, in.sel_t, nbits, c.st2);
+      r1.push_back(commit_launch(c, sTc, n, slot++, 1));
+    } else {
+      wait_input(2 * k, c.st);
+      intt_nat(c, sFc, in.sel_f, nbits);
+      wait_input(2 * k + 1, c.st);
+      intt_nat(c, sTc, in.sel_t, nbits);
+    }
   }
-  std::vector<Commit> r1;
-  int slot = 0;
-  fork_lanes(c);
-  for (int i = 0; i < k; i++) {
-    r1.push_back(commit_launch(c, Fc[i], n, slot++, 0));
-    r1.push_back(commit_launch(c, Tc[i], n, slot++, 1));
-  }
-  if (sel) {
-    r1.push_back(commit_launch(c, sFc, n, slot++, 0));
-    r1.push_back(commit_launch(c, sTc, n, slot++, 1));
+  if (!piped) {
+    fork_lanes(c);
+    for (int i = 0; i < k; i++) {
+      r1.push_back(commit_launch(c, Fc[i], n, slot++, 0));
+      r1.push_back(commit_launch(c, Tc[i], n, slot++, 1));
+    }
+    if (sel) {
+      r1.push_back(commit_launch(c, sFc, n, slot++, 0));
+      r1.push_back(commit_launch(c, sTc, n, slot++, 1));
+    }
   }
   c.sync();
   if (in.after_round1) in.after_round1();
@@ -1232,6 +1277,16 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   }
   using hclk = std::chrono::steady_clock;
   const auto h0 = hclk::now();
+  struct Feeder {  // the input-copy thread of vectors 1.. (joined on every exit path)
+    std::thread t;
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t issued = 1;
+    std::exception_ptr err;
+    ~Feeder() {
+      if (t.joinable()) t.join();
+    }
+  } feeder;
   Range rin("kgs.host.input_copy");
   if (ctx->group) {  // the distributed prover reads every input at once
     par_copy(in_jobs);
@@ -1253,15 +1308,36 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
       ctx->ev_in.push_back(e);
     }
     in.ready.assign(in_jobs.size(), nullptr);
-    for (size_t v = 0; v < in_jobs.size(); v++) {
-      par_copy({in_jobs[v]});
-      if (v == 0) {
-        HC(hipMemcpyAsync(dsts[v], in_jobs[v].dst, E, hipMemcpyHostToDevice, ctx->st));
-      } else {
-        HC(hipMemcpyAsync(dsts[v], in_jobs[v].dst, E, hipMemcpyHostToDevice, ctx->st_copy));
-        HC(hipEventRecord(ctx->ev_in[v], ctx->st_copy));
-        in.ready[v] = ctx->ev_in[v];
-      }
+    par_copy({in_jobs[0]});
+    HC(hipMemcpyAsync(dsts[0], in_jobs[0].dst, E, hipMemcpyHostToDevice, ctx->st));
+    for (size_t v = 1; v < in_jobs.size(); v++) in.ready[v] = ctx->ev_in[v];
+    // vectors 1.. are copied into their pinned slots and DMA'd by a feeder thread while the prover
+    // already enqueues (and the GPU runs) vector 0's work; prove_impl waits for a vector's DMA to be
+    // ENQUEUED (input_issued) before its kernels wait on the vector's event
+    if (in_jobs.size() > 1) {
+      feeder.t = std::thread([&, dev = ctx->device] {
+        try {
+          HC(hipSetDevice(dev));
+          for (size_t v = 1; v < in_jobs.size(); v++) {
+            par_copy({in_jobs[v]});
+            HC(hipMemcpyAsync(dsts[v], in_jobs[v].dst, E, hipMemcpyHostToDevice, ctx->st_copy));
+            HC(hipEventRecord(ctx->ev_in[v], ctx->st_copy));
+            std::lock_guard<std::mutex> lk(feeder.mu);
+            feeder.issued = v + 1;
+            feeder.cv.notify_all();
+          }
+        } catch (...) {
+          std::lock_guard<std::mutex> lk(feeder.mu);
+          feeder.err = std::current_exception();
+          feeder.issued = in_jobs.size();
+          feeder.cv.notify_all();
+        }
+      });
+      in.input_issued = [&](size_t v) {
+        std::unique_lock<std::mutex> lk(feeder.mu);
+        feeder.cv.wait(lk, [&] { return feeder.issued > v; });
+        if (feeder.err) std::rethrow_exception(feeder.err);
+      };
     }
   }
   rin.pop();
