@@ -718,7 +718,10 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
       r1.push_back(commit_launch(c, sTc, n, slot++, 1));
     }
   }
-  c.sync();
+  // round 1's commitments only: the Montgomery write-back on the copy stream keeps running under
+  // rounds 2-5 (in.after_round1's thread waits for it before copying to the caller)
+  HC(hipStreamSynchronize(c.st));
+  if (c.st2) HC(hipStreamSynchronize(c.st2));
   if (in.after_round1) in.after_round1();
   const int ncom = 2 * k + (sel ? 2 : 0) + 4;
   std::vector<std::vector<uint8_t>> com(ncom, std::vector<uint8_t>(64));
@@ -1277,6 +1280,16 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   }
   using hclk = std::chrono::steady_clock;
   const auto h0 = hclk::now();
+  // each vector in pieces: the host copy of piece p + 1 into the pinned slot runs while piece p is
+  // DMA'd, so a vector's DMA ends one piece after its host copy instead of a whole vector after
+  const size_t piece = (size_t)8 << 20;
+  auto feed = [&](size_t v, hipStream_t st) {
+    for (size_t o = 0; o < E; o += piece) {
+      const size_t len = std::min(piece, E - o);
+      par_copy({{in_jobs[v].dst + o, in_jobs[v].src + o, len}});
+      HC(hipMemcpyAsync((uint8_t*)dsts[v] + o, in_jobs[v].dst + o, len, hipMemcpyHostToDevice, st));
+    }
+  };
   struct Feeder {  // the input-copy thread of vectors 1.. (joined on every exit path)
     std::thread t;
     std::mutex mu;
@@ -1308,8 +1321,7 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
       ctx->ev_in.push_back(e);
     }
     in.ready.assign(in_jobs.size(), nullptr);
-    par_copy({in_jobs[0]});
-    HC(hipMemcpyAsync(dsts[0], in_jobs[0].dst, E, hipMemcpyHostToDevice, ctx->st));
+    feed(0, ctx->st);
     for (size_t v = 1; v < in_jobs.size(); v++) in.ready[v] = ctx->ev_in[v];
     // vectors 1.. are copied into their pinned slots and DMA'd by a feeder thread while the prover
     // already enqueues (and the GPU runs) vector 0's work; prove_impl waits for a vector's DMA to be
@@ -1319,8 +1331,7 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
         try {
           HC(hipSetDevice(dev));
           for (size_t v = 1; v < in_jobs.size(); v++) {
-            par_copy({in_jobs[v]});
-            HC(hipMemcpyAsync(dsts[v], in_jobs[v].dst, E, hipMemcpyHostToDevice, ctx->st_copy));
+            feed(v, ctx->st_copy);
             HC(hipEventRecord(ctx->ev_in[v], ctx->st_copy));
             std::lock_guard<std::mutex> lk(feeder.mu);
             feeder.issued = v + 1;
@@ -1361,16 +1372,28 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   }
   struct Joiner {
     std::thread t;
+    bool failed = false;
     ~Joiner() {
       if (t.joinable()) t.join();
     }
   } out_copy;
-  if (!out_jobs.empty()) in.after_round1 = [&] { out_copy.t = std::thread([&] { par_copy(out_jobs); }); };
+  if (!out_jobs.empty())
+    in.after_round1 = [&] {
+      out_copy.t = std::thread([&, dev = ctx->device] {
+        // the device -> pinned write-back (copy stream) must be complete before the pinned -> caller copy
+        if (hipSetDevice(dev) != hipSuccess || hipStreamSynchronize(ctx->st_copy) != hipSuccess) {
+          out_copy.failed = true;
+          return;
+        }
+        par_copy(out_jobs);
+      });
+    };
   const auto h2 = hclk::now();
   prove_impl(*ctx, in, commitments_out, evaluations_out);  // ends synchronised
   const auto h3 = hclk::now();
   Range rout("kgs.host.writeback_wait");
   if (out_copy.t.joinable()) out_copy.t.join();
+  if (out_copy.failed) throw KgsError(KGS_E_HIP, "Montgomery write-back: copy stream failed");
   rout.pop();
   const auto h4 = hclk::now();
   // host-boundary phases: [6] input copy into pinned staging, [7] prover, [8] write-back wait
