@@ -41,6 +41,7 @@ function perDevice() {
 }
 
 const pool = { slots: [], idle: [], waiters: [], devs: null, cap: 0 };
+const diag = { execMs: null, timing: null };
 
 function newSlot() {
     if (!pool.devs) {
@@ -110,7 +111,11 @@ async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT) {
     return withContext(async slot => {
         await load().srsLoadPtau(slot.ctx, key, nBits);
         setLanes(slot);
-        return load().prove(slot.ctx, kind, nBits, evalsF, evalsT, selF, selT);
+        const res = await load().prove(slot.ctx, kind, nBits, evalsF, evalsT, selF, selT);
+        // diagnostics of the last call (time inside libkgs; kgs_last_timing rounds / copy / prover / write-back)
+        diag.execMs = res.execMs;
+        diag.timing = load().lastTiming(slot.ctx);
+        return res;
     });
 }
 
@@ -166,4 +171,4 @@ function poolInfo() {
              idle: pool.idle.length, waiting: pool.waiters.length };
 }
 
-module.exports = { load, ptauPower, prove, withContext, poolInfo, GRANDSUM: 0, GRANDPRODUCT: 1, LOOKUP: 2 };
+module.exports = { load, ptauPower, prove, withContext, poolInfo, diag, GRANDSUM: 0, GRANDPRODUCT: 1, LOOKUP: 2 };
