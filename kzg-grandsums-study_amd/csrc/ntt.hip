@@ -183,7 +183,10 @@ static inline unsigned nblocks(uint64_t work, unsigned bs = 256) { return (unsig
 // 2^21 pair 0.625 -> 0.616 ms (same-box A/B, profiles/r03/ntt_ab.txt): LDS was never the limiter —
 // the pass waves sit 37-41 % of their cycles parked on global loads and barriers at 2 blocks (8 waves)
 // per CU. Tile size: 2^11 elements (64 KiB, 256 threads); 2^10-element tiles with 128 threads
-// (-DKGS_NTT_ELOG=10: five blocks per CU) measured 16 % slower.
+// (-DKGS_NTT_ELOG=10: five blocks per CU) measured 16 % slower. A persistent grid (two blocks per CU
+// walking the tiles) that prefetches the next tile's elements into registers during the rounds was
+// measured too and rejected: 2^21 pair 0.609 ms (this kernel) vs 0.627 (persistent, no prefetch),
+// 0.636 (2 of 8 elements prefetched), 0.655 (4 of 8: register spills), profiles/r03/ntt_pf_ab.txt.
 #ifndef KGS_NTT_ELOG
 #define KGS_NTT_ELOG 11
 #endif
@@ -321,100 +324,6 @@ __global__ void __launch_bounds__(LDS_NT) k_ntt_lds_pass(uint32_t* __restrict__ 
   }
 }
 
-#ifndef KGS_NTT_PF_ELEMS
-#define KGS_NTT_PF_ELEMS 4
-#endif
-// Persistent form of the same pass (-DKGS_NTT_PF; the default is the one-tile-per-block kernel
-// above): a grid of at most two blocks per CU (the 64 KiB tile allows two per CU) walks the tiles with
-// stride gridDim.x and loads tile t + gridDim.x into registers (8 elements per thread) right after
-// tile t is staged in LDS, so that load's latency runs under tile t's two register rounds instead
-// of leaving the block parked on it (the one-tile kernel's waves sat 37-41 % of their cycles in
-// s_waitcnt / barriers: profiles/r03/ntt_counters.txt). Same loads, butterflies, twiddles and
-// stores in the same places: bit-identical.
-template <int K1, int K2, bool DIT>
-__global__ void __launch_bounds__(LDS_NT, 2) k_ntt_lds_pass_pf(uint32_t* __restrict__ data, const uint32_t* __restrict__ in,
-                                                         uint64_t in_len, int in_bitrev, const uint32_t* __restrict__ pre,
-                                                         const uint32_t* __restrict__ tw, int logm, int s0,
-                                                         const uint32_t* __restrict__ post,
-                                                         const uint32_t* __restrict__ post_s, uint32_t ntiles) {
-  KGS_AUX_PRIO();
-  constexpr int K = K1 + K2;
-  constexpr int LBLOG = NTT_ELOG - K;
-  constexpr int LB = 1 << LBLOG;
-  constexpr int EPT = LDS_ELEMS / LDS_NT;
-  constexpr int PF = KGS_NTT_PF_ELEMS;  // of a thread's EPT elements, the first PF are prefetched
-  __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_ELEMS * 8];
-  const int logd = DIT ? s0 : logm - s0 - K;
-  uint32_t tile = blockIdx.x;
-  if (tile >= ntiles) return;  // uniform per block
-  auto ld = [&](uint64_t idx) {
-    if (in) {
-      if (DIT) return fr::load(in + 8 * (in_bitrev ? idx : (uint64_t)bitrev((uint32_t)idx, logm)));
-      return idx < in_len ? fr::load(in + 8 * idx) : fr::zero();
-    }
-    return fr::load(data + 8 * idx);
-  };
-  fr pf[PF > 0 ? PF : 1];
-  auto fetch = [&](uint32_t t) {
-    const uint64_t c0 = (uint64_t)t * LB;
-#pragma unroll
-    for (int r = 0; r < PF; r++) {
-      uint32_t j, cl;
-      lds_map(threadIdx.x + r * LDS_NT, K, logd, LBLOG, j, cl);
-      pf[r] = ld(lds_idx(c0 + cl, j, K, logd));
-    }
-  };
-  fetch(tile);
-  for (;;) {
-    const uint64_t col0 = (uint64_t)tile * LB;
-#pragma unroll
-    for (int r = 0; r < EPT; r++) {
-      uint32_t j, cl;
-      lds_map(threadIdx.x + r * LDS_NT, K, logd, LBLOG, j, cl);
-      fr x = r < PF ? pf[r] : ld(lds_idx(col0 + cl, j, K, logd));
-      if (!DIT && in && pre) {
-        const uint64_t idx = lds_idx(col0 + cl, j, K, logd);
-        if (idx < in_len) x = x * fr::load(pre + 8 * idx);
-      }
-      lds_st(lds, j * LB + cl, x);
-    }
-    __syncthreads();
-    const uint32_t next = tile + gridDim.x;
-    if (next < ntiles) fetch(next);  // in flight during the rounds below
-    for (uint32_t g = threadIdx.x; g < (LDS_ELEMS >> K1); g += LDS_NT) {
-      const uint32_t cl = g & (LB - 1), jq = g >> LBLOG;
-      if (DIT)
-        lds_round<K1, true>(lds, tw, cl, col0 + cl, jq << K1, 1, K, logd, LB, 0);
-      else
-        lds_round<K1, false>(lds, tw, cl, col0 + cl, jq, 1u << K2, K, logd, LB, 0);
-    }
-    __syncthreads();
-    for (uint32_t g = threadIdx.x; g < (LDS_ELEMS >> K2); g += LDS_NT) {
-      const uint32_t cl = g & (LB - 1), jq = g >> LBLOG;
-      if (DIT)
-        lds_round<K2, true>(lds, tw, cl, col0 + cl, jq, 1u << K1, K, logd, LB, K1);
-      else
-        lds_round<K2, false>(lds, tw, cl, col0 + cl, jq << K2, 1, K, logd, LB, K1);
-    }
-    __syncthreads();
-    fr ps;
-    if (post_s) ps = fr::load(post_s);
-#pragma unroll
-    for (int r = 0; r < EPT; r++) {
-      uint32_t j, cl;
-      lds_map(threadIdx.x + r * LDS_NT, K, logd, LBLOG, j, cl);
-      const uint64_t idx = lds_idx(col0 + cl, j, K, logd);
-      fr y = lds_ld(lds, j * LB + cl);
-      if (post) y = y * fr::load(post + 8 * idx);
-      if (post_s) y = y * ps;
-      canon_out(y).store(data + 8 * idx);
-    }
-    if (next >= ntiles) break;
-    tile = next;
-    __syncthreads();  // every lane has read its tile out of LDS before the next one is staged
-  }
-}
-
 #ifndef KGS_NO_NTT_LDS
 // stages per pass for m = 2^logm: LDS passes of up to 6 stages while >= 4 remain, radix-8/4/2 after
 static inline int lds_pass_stages(int left) { return left >= 6 ? 6 : left >= 4 ? left : 0; }
@@ -424,23 +333,10 @@ constexpr int LDS_MIN_LOGM = NTT_ELOG > 11 ? NTT_ELOG : 11;
 static void launch_lds_pass(hipStream_t st, int K, bool dit, uint32_t* data, const uint32_t* in, uint64_t in_len,
                             int in_bitrev, const uint32_t* pre, const uint32_t* tw, int logm, int s0,
                             const uint32_t* post, const uint32_t* post_s) {
-  const unsigned tiles = (unsigned)((1ull << logm) / LDS_ELEMS);
-#ifndef KGS_NTT_PF
+  const unsigned blocks = (unsigned)((1ull << logm) / LDS_ELEMS);
 #define KGS_LDS_LAUNCH(A, B, D)                                                                                  \
-  hipLaunchKernelGGL((k_ntt_lds_pass<A, B, D>), dim3(tiles), dim3(LDS_NT), 0, st, data, in, in_len, in_bitrev, pre, \
+  hipLaunchKernelGGL((k_ntt_lds_pass<A, B, D>), dim3(blocks), dim3(LDS_NT), 0, st, data, in, in_len, in_bitrev, pre, \
                      tw, logm, s0, post, post_s)
-#else
-  static const unsigned cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    return (unsigned)n;
-  }();
-  const unsigned per_cu = (160u << 10) / (LDS_ELEMS * 32u);  // tiles resident per CU (LDS-limited)
-  const unsigned blocks = std::min(tiles, cus * (per_cu ? per_cu : 1u));
-#define KGS_LDS_LAUNCH(A, B, D)                                                                                     \
-  hipLaunchKernelGGL((k_ntt_lds_pass_pf<A, B, D>), dim3(blocks), dim3(LDS_NT), 0, st, data, in, in_len, in_bitrev, pre, \
-                     tw, logm, s0, post, post_s, tiles)
-#endif
   if (dit) {
     if (K == 6) KGS_LDS_LAUNCH(3, 3, true); else if (K == 5) KGS_LDS_LAUNCH(3, 2, true); else KGS_LDS_LAUNCH(2, 2, true);
   } else {

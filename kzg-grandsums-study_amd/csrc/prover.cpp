@@ -1209,13 +1209,59 @@ int kgs_ptau_write_synthetic(kgs_ctx_t* ctx, const char* path, int power, const 
 namespace kgsi {
 // host copies between pageable caller buffers and the pinned staging area, split over threads; the
 // 16 threads (a GPU's host share) are divided among the contexts copying at the same time, so that
-// several proofs in flight through the host-buffer boundary do not oversubscribe the cores
+// several proofs in flight through the host-buffer boundary do not oversubscribe the cores. The
+// helpers are a persistent pool (spawning 8-16 threads per call cost ~0.1 ms, paid several times per
+// proof once inputs are fed in pieces); the calling thread copies too, so a busy pool never stalls it.
 static std::atomic<int> g_copy_active{0};
+namespace {
+struct CopyTask {
+  std::vector<CopyJob> pieces;
+  std::atomic<size_t> next{0}, done{0};
+  std::mutex mu;
+  std::condition_variable cv;
+  void work() {
+    size_t i, mine = 0;
+    while ((i = next.fetch_add(1)) < pieces.size()) {
+      memcpy(pieces[i].dst, pieces[i].src, pieces[i].len);
+      mine++;
+    }
+    if (mine && done.fetch_add(mine) + mine == pieces.size()) {
+      std::lock_guard<std::mutex> lk(mu);
+      cv.notify_all();
+    }
+  }
+};
+struct CopyPool {  // leaked on purpose: its detached threads outlive static destruction
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::shared_ptr<CopyTask>> q;
+  explicit CopyPool(unsigned n) {
+    for (unsigned t = 0; t < n; t++)
+      std::thread([this] {
+        for (;;) {
+          std::shared_ptr<CopyTask> task;
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return !q.empty(); });
+            task = std::move(q.back());
+            q.pop_back();
+          }
+          task->work();
+        }
+      }).detach();
+  }
+  static CopyPool& get() {
+    static CopyPool* p = new CopyPool(16);
+    return *p;
+  }
+};
+}  // namespace
+
 void par_copy(const std::vector<CopyJob>& jobs) {
   const size_t piece = 1u << 20;
-  std::vector<CopyJob> pieces;
+  auto task = std::make_shared<CopyTask>();
   for (const auto& j : jobs)
-    for (size_t o = 0; o < j.len; o += piece) pieces.push_back({j.dst + o, j.src + o, std::min(piece, j.len - o)});
+    for (size_t o = 0; o < j.len; o += piece) task->pieces.push_back({j.dst + o, j.src + o, std::min(piece, j.len - o)});
   struct Active {
     int n;
     Active() : n(g_copy_active.fetch_add(1) + 1) {}
@@ -1223,21 +1269,102 @@ void par_copy(const std::vector<CopyJob>& jobs) {
   } active;
   unsigned nth = std::thread::hardware_concurrency();
   nth = std::max(1u, std::min(nth, 16u) / (unsigned)std::max(1, active.n));
-  if (pieces.size() < 2 || nth == 1) {
-    for (const auto& p : pieces) memcpy(p.dst, p.src, p.len);
-    return;
+  nth = std::min<unsigned>(nth, (unsigned)task->pieces.size());
+  if (nth > 1) {
+    CopyPool& pool = CopyPool::get();
+    {
+      std::lock_guard<std::mutex> lk(pool.mu);
+      for (unsigned t = 1; t < nth; t++) pool.q.push_back(task);  // helpers; this thread is the nth
+    }
+    pool.cv.notify_all();
   }
-  nth = std::min<unsigned>(nth, (unsigned)pieces.size());
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nth; t++)
-    th.emplace_back([&, t] {
-      for (size_t i = t; i < pieces.size(); i += nth) memcpy(pieces[i].dst, pieces[i].src, pieces[i].len);
-    });
-  for (auto& x : th) x.join();
+  task->work();
+  std::unique_lock<std::mutex> lk(task->mu);
+  task->cv.wait(lk, [&] { return task->done.load() == task->pieces.size(); });
 }
+
+// Caller buffers pinned in place for the duration of one kgs_prove (hipHostRegister: ~0.1 ms per
+// 32 MiB, profiles/r03/hostreg.txt, against ~1 ms to copy the same bytes into pinned staging), so
+// the DMAs read / write the caller's memory directly. Memory the caller already pinned
+// (hipHostMalloc, kgs_host_register) is used as it is and left alone. Registrations are released
+// after every stream of the context is drained (also on an error path).
+// Concurrent calls may pass the same buffer (e.g. one selector vector shared by several proofs): the
+// registrations are reference-counted process-wide, so the first call to finish does not unpin memory
+// another call is still DMA-ing. Overlapping buffers with different starts fail to register and take
+// the staging path.
+static std::mutex g_pin_mu;
+static std::map<void*, std::pair<size_t, int>> g_pins;  // start -> (bytes, calls holding it)
+struct HostPins {
+  kgs_ctx* ctx;
+  std::vector<void*> mine;
+  explicit HostPins(kgs_ctx* c) : ctx(c) {}
+  static bool pinned_elsewhere(const void* p) {
+    hipPointerAttribute_t a{};
+    const bool ok = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
+    (void)hipGetLastError();  // a pageable pointer is an error here: not a sticky launch error
+    return ok;
+  }
+  bool pin(const void* cp, size_t n) {
+    void* p = const_cast<void*>(cp);
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pins.find(p);
+    if (it != g_pins.end()) {
+      if (it->second.first < n) return false;
+      it->second.second++;
+      mine.push_back(p);
+      return true;
+    }
+    if (pinned_elsewhere(p)) return true;  // the caller's own pinned memory: use, never unpin
+    if (getenv("KGS_NO_HOST_REGISTER")) return false;  // A/B: the pinned-staging copy path
+    if (hipHostRegister(p, n, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    g_pins[p] = {n, 1};
+    mine.push_back(p);
+    return true;
+  }
+  static void drop(void* p) {  // under g_pin_mu
+    auto it = g_pins.find(p);
+    if (it != g_pins.end() && --it->second.second == 0) {
+      hipHostUnregister(p);
+      g_pins.erase(it);
+    }
+  }
+  void release_from(size_t k) {  // the pins made after the first k (no DMA issued on them yet)
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    while (mine.size() > k) {
+      drop(mine.back());
+      mine.pop_back();
+    }
+  }
+  ~HostPins() {
+    if (mine.empty()) return;
+    hipSetDevice(ctx->device);
+    if (ctx->st) hipStreamSynchronize(ctx->st);
+    if (ctx->st2) hipStreamSynchronize(ctx->st2);
+    if (ctx->st_copy) hipStreamSynchronize(ctx->st_copy);
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    for (void* p : mine) drop(p);
+  }
+};
 }  // namespace kgsi
 
 extern "C" {
+
+int kgs_host_register(void* ptr, uint64_t bytes) {
+  API_BEGIN
+  if (!ptr || !bytes) throw KgsError(KGS_E_ARG, "NULL argument");
+  HC(hipHostRegister(ptr, (size_t)bytes, hipHostRegisterDefault));
+  API_END
+}
+
+int kgs_host_unregister(void* ptr) {
+  API_BEGIN
+  if (!ptr) throw KgsError(KGS_E_ARG, "NULL argument");
+  HC(hipHostUnregister(ptr));
+  API_END
+}
 
 int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* const* evals_f,
               const uint8_t* const* evals_t, const uint8_t* sel_f, const uint8_t* sel_t, uint8_t* const* mont_f,
@@ -1301,7 +1428,30 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
     }
   } feeder;
   Range rin("kgs.host.input_copy");
-  if (ctx->group) {  // the distributed prover reads every input at once
+  HostPins pins(ctx);  // declared after the feeder: released only once every stream is drained
+  bool direct = !ctx->group;
+  for (size_t v = 0; direct && v < in_jobs.size(); v++) direct = pins.pin(in_jobs[v].src, E);
+  if (!direct) pins.release_from(0);
+  if (direct) {
+    // zero-copy: every input DMA'd straight from the caller's (now pinned) buffer; vector 0 on the
+    // main stream, the others on the copy stream with the event their first kernel waits for
+    if (!ctx->st_copy) {
+      HC(hipStreamCreateWithFlags(&ctx->st_copy, hipStreamNonBlocking));
+      HC(hipEventCreateWithFlags(&ctx->ev_copy, hipEventDisableTiming));
+    }
+    while (ctx->ev_in.size() < in_jobs.size()) {
+      hipEvent_t e;
+      HC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ctx->ev_in.push_back(e);
+    }
+    in.ready.assign(in_jobs.size(), nullptr);
+    HC(hipMemcpyAsync(dsts[0], in_jobs[0].src, E, hipMemcpyHostToDevice, ctx->st));
+    for (size_t v = 1; v < in_jobs.size(); v++) {
+      HC(hipMemcpyAsync(dsts[v], in_jobs[v].src, E, hipMemcpyHostToDevice, ctx->st_copy));
+      HC(hipEventRecord(ctx->ev_in[v], ctx->st_copy));
+      in.ready[v] = ctx->ev_in[v];
+    }
+  } else if (ctx->group) {  // the distributed prover reads every input at once
     par_copy(in_jobs);
     for (size_t v = 0; v < in_jobs.size(); v++)
       HC(hipMemcpyAsync(dsts[v], in_jobs[v].dst, E, hipMemcpyHostToDevice, ctx->st));
@@ -1353,11 +1503,18 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   }
   rin.pop();
   const auto h1 = hclk::now();
+  // the Montgomery write-back: D2H straight into the caller's buffer once it is pinned (the JS addon
+  // keeps its recycled output buffers registered), else into the pinned slot + a host copy
+  std::vector<bool> wb_direct(2 * npols, false);
   for (int i = 0; i < npols; i++) {
     in.f_std.push_back(dsts[2 * i]);
     in.t_std.push_back(dsts[2 * i + 1]);
-    in.mont_f_out.push_back(mont_f && mont_f[i] ? pio + (size_t)(2 * i) * E : nullptr);
-    in.mont_t_out.push_back(mont_t && mont_t[i] ? pio + (size_t)(2 * i + 1) * E : nullptr);
+    const bool fd = mont_f && mont_f[i] && !ctx->group && pins.pin(mont_f[i], E);
+    const bool td = mont_t && mont_t[i] && !ctx->group && pins.pin(mont_t[i], E);
+    wb_direct[2 * i] = fd;
+    wb_direct[2 * i + 1] = td;
+    in.mont_f_out.push_back(mont_f && mont_f[i] ? (fd ? mont_f[i] : pio + (size_t)(2 * i) * E) : nullptr);
+    in.mont_t_out.push_back(mont_t && mont_t[i] ? (td ? mont_t[i] : pio + (size_t)(2 * i + 1) * E) : nullptr);
   }
   if (sel_f) {
     in.sel_f = dsts[2 * npols];
@@ -1367,8 +1524,8 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   // caller on a host thread while rounds 2-5 run
   std::vector<CopyJob> out_jobs;
   for (int i = 0; i < npols; i++) {
-    if (mont_f && mont_f[i]) out_jobs.push_back({mont_f[i], pio + (size_t)(2 * i) * E, E});
-    if (mont_t && mont_t[i]) out_jobs.push_back({mont_t[i], pio + (size_t)(2 * i + 1) * E, E});
+    if (mont_f && mont_f[i] && !wb_direct[2 * i]) out_jobs.push_back({mont_f[i], pio + (size_t)(2 * i) * E, E});
+    if (mont_t && mont_t[i] && !wb_direct[2 * i + 1]) out_jobs.push_back({mont_t[i], pio + (size_t)(2 * i + 1) * E, E});
   }
   struct Joiner {
     std::thread t;

@@ -125,6 +125,9 @@ uint8_t* out_alloc(size_t len) {
   const uintptr_t end = (uintptr_t)raw + sz + HUGE;
   if (end > a + sz) munmap((void*)(a + sz), end - (a + sz));
   madvise((void*)a, sz, MADV_HUGEPAGE);
+  // pinned for the whole life of the buffer: kgs_prove then DMAs the Montgomery write-back straight
+  // into it (no per-call registration, no staging copy); unpinned before it is unmapped
+  kgs_host_register((void*)a, sz);
   return (uint8_t*)a;
 }
 
@@ -138,6 +141,7 @@ void out_release(uint8_t* p, size_t len) {
       return;
     }
   }
+  kgs_host_unregister(p);
   munmap(p, sz);
 }
 }  // namespace
