@@ -181,11 +181,11 @@ int kgs_ptau_write_synthetic(kgs_ctx_t* ctx, const char* path, int power, const 
 int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* const* evals_f,
               const uint8_t* const* evals_t, const uint8_t* sel_f, const uint8_t* sel_t, uint8_t* const* mont_f,
               uint8_t* const* mont_t, uint8_t* commitments_out, uint8_t* evaluations_out);
-/* Host-buffer boundary: kgs_prove pins the caller's input and output buffers in place for the call
- * (hipHostRegister) and DMAs them directly — no staging copy — falling back to pinned staging when a
- * buffer cannot be registered. A caller that reuses its buffers across proofs (the JS addon's
- * recycled output buffers) can keep them pinned with kgs_host_register, which makes the per-call
- * registration free; kgs_host_unregister before freeing such a buffer. */
+/* Host-buffer boundary: kgs_prove copies pageable inputs into pinned staging (pieces overlapped with
+ * their DMA) and the Montgomery outputs back out of it. Buffers the caller has pinned — hipHostMalloc
+ * or kgs_host_register, for buffers reused across proofs — are DMA'd in place with no staging copy;
+ * kgs_host_unregister before freeing a registered buffer. Registration costs more than one copy
+ * (profiles/r03/boundary_ab.txt): register only buffers that outlive several proofs. */
 int kgs_host_register(void* ptr, uint64_t bytes);
 int kgs_host_unregister(void* ptr);
 /* Same with device-resident inputs (HIP device pointers on ctx's device). */

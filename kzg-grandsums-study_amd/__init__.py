@@ -70,6 +70,8 @@ def lib():
                                        ctypes.c_void_p, ctypes.c_void_p, c_u8p, c_u8p]
         L.kgs_proof_shape.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                       ctypes.POINTER(ctypes.c_int)]
+        L.kgs_host_register.argtypes = [c_u8p, ctypes.c_uint64]
+        L.kgs_host_unregister.argtypes = [c_u8p]
         L.kgs_last_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.kgs_fr_to_mont.argtypes = [ctypes.c_void_p, c_u8p, c_u8p, ctypes.c_uint64]
         L.kgs_fr_from_mont.argtypes = [ctypes.c_void_p, c_u8p, c_u8p, ctypes.c_uint64]
@@ -169,6 +171,21 @@ def device_count():
     n = ctypes.c_int()
     _check(lib().kgs_device_count(ctypes.byref(n)))
     return n.value
+
+
+def host_register(buf):
+    """Pin a writable host buffer (bytearray / numpy) that several proofs will reuse: kgs_prove then
+    DMAs it in place instead of through pinned staging (kgs_host_register). Returns a handle to pass
+    to host_unregister before the buffer is released or resized."""
+    p, keep = _ptr(buf)
+    if isinstance(keep, ctypes.Array):
+        raise TypeError("host_register needs a writable buffer (bytearray, numpy array)")
+    _check(lib().kgs_host_register(p, len(buf)))
+    return p, keep
+
+
+def host_unregister(handle):
+    _check(lib().kgs_host_unregister(handle[0]))
 
 
 def shard_range(n, rank, world):

@@ -1283,15 +1283,17 @@ void par_copy(const std::vector<CopyJob>& jobs) {
   task->cv.wait(lk, [&] { return task->done.load() == task->pieces.size(); });
 }
 
-// Caller buffers pinned in place for the duration of one kgs_prove (hipHostRegister: ~0.1 ms per
-// 32 MiB, profiles/r03/hostreg.txt, against ~1 ms to copy the same bytes into pinned staging), so
-// the DMAs read / write the caller's memory directly. Memory the caller already pinned
-// (hipHostMalloc, kgs_host_register) is used as it is and left alone. Registrations are released
-// after every stream of the context is drained (also on an error path).
-// Concurrent calls may pass the same buffer (e.g. one selector vector shared by several proofs): the
-// registrations are reference-counted process-wide, so the first call to finish does not unpin memory
-// another call is still DMA-ing. Overlapping buffers with different starts fail to register and take
-// the staging path.
+// Caller buffers the DMAs can read / write in place: memory the caller already pinned (hipHostMalloc,
+// kgs_host_register) is used as it is and left alone, so a caller that keeps its buffers across
+// proofs skips the staging copy. Registering pageable buffers per call (KGS_HOST_REGISTER=1) is kept
+// as an opt-in only: measured at 2^20 it makes the host path slower, 21.5 vs 16.0 ms per proof, and
+// the JS concurrent rate 44.9 vs 78.8 proofs/s (register + unregister of 2 x 32 MiB costs more than
+// the ~1 ms copy it saves, and registrations serialise across contexts), profiles/r03/boundary_ab.txt.
+// Per-call registrations are released after every stream of the context is drained (also on an error
+// path). Concurrent calls may pass the same buffer (e.g. one selector vector shared by several
+// proofs): the registrations are reference-counted process-wide, so the first call to finish does not
+// unpin memory another call is still DMA-ing. Overlapping buffers with different starts fail to
+// register and take the staging path.
 static std::mutex g_pin_mu;
 static std::map<void*, std::pair<size_t, int>> g_pins;  // start -> (bytes, calls holding it)
 struct HostPins {
@@ -1315,7 +1317,8 @@ struct HostPins {
       return true;
     }
     if (pinned_elsewhere(p)) return true;  // the caller's own pinned memory: use, never unpin
-    if (getenv("KGS_NO_HOST_REGISTER")) return false;  // A/B: the pinned-staging copy path
+    static const bool reg = getenv("KGS_HOST_REGISTER") != nullptr;  // opt-in, see above
+    if (!reg) return false;
     if (hipHostRegister(p, n, hipHostRegisterDefault) != hipSuccess) {
       (void)hipGetLastError();
       return false;

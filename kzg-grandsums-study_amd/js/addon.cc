@@ -127,7 +127,8 @@ uint8_t* out_alloc(size_t len) {
   madvise((void*)a, sz, MADV_HUGEPAGE);
   // pinned for the whole life of the buffer: kgs_prove then DMAs the Montgomery write-back straight
   // into it (no per-call registration, no staging copy); unpinned before it is unmapped
-  kgs_host_register((void*)a, sz);
+  static const bool no_reg = getenv("KGS_JS_NO_OUT_REGISTER") != nullptr;  // A/B switch
+  if (!no_reg) kgs_host_register((void*)a, sz);
   return (uint8_t*)a;
 }
 
@@ -141,7 +142,8 @@ void out_release(uint8_t* p, size_t len) {
       return;
     }
   }
-  kgs_host_unregister(p);
+  static const bool no_reg = getenv("KGS_JS_NO_OUT_REGISTER") != nullptr;
+  if (!no_reg) kgs_host_unregister(p);
   munmap(p, sz);
 }
 }  // namespace

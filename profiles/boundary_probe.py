@@ -1,5 +1,6 @@
 """Host-buffer boundary vs device-resident latency of one grand-sum proof (one context, two MSM lanes),
 round by round (kgs_last_timing): where the drop-in path's extra milliseconds go.
+host_prereg: inputs pinned once by the caller (kgs_host_register), DMA'd in place.
 usage: python profiles/boundary_probe.py [nbits=20] [reps=5]"""
 import os
 import sys
@@ -31,10 +32,14 @@ def main():
     for _ in range(2):
         ctx.prove(K.GRANDSUM, nbits, hf, ht)
         ctx.prove_device(K.GRANDSUM, nbits, [df.data_ptr()], [dt.data_ptr()])
+    # the same vectors in buffers the caller pinned once (kgs_host_register): DMA'd in place
+    rf, rt = [bytearray(f.tobytes())], [bytearray(t.tobytes())]
+    handles = [K.host_register(b) for b in rf + rt]
     fmt = lambda xs: " ".join(f"{x:6.2f}" for x in xs)  # noqa: E731
     for label, fn in (("device", lambda: ctx.prove_device(K.GRANDSUM, nbits, [df.data_ptr()], [dt.data_ptr()])),
                       ("host", lambda: ctx.prove(K.GRANDSUM, nbits, hf, ht)),
-                      ("host_no_mont", lambda: ctx.prove(K.GRANDSUM, nbits, hf, ht, mont_out=False))):
+                      ("host_no_mont", lambda: ctx.prove(K.GRANDSUM, nbits, hf, ht, mont_out=False)),
+                      ("host_prereg", lambda: ctx.prove(K.GRANDSUM, nbits, rf, rt, mont_out=False))):
         for _ in range(reps):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -43,6 +48,8 @@ def main():
             tm = ctx.last_timing()
             print(f"{label:13s} {el:7.2f} ms | rounds {fmt(tm[:5])} | copy/prove/wb {fmt(tm[6:9]) if len(tm) > 6 else ''}",
                   flush=True)
+    for h in handles:
+        K.host_unregister(h)
 
 
 if __name__ == "__main__":

@@ -318,6 +318,38 @@ def test_mid_size_vs_c_oracle(K, kind, nbits, npols, sel):
     ctx.close()
 
 
+@pytest.mark.parametrize("which", ["all", "some"])
+def test_caller_pinned_inputs(K, which):
+    """Inputs the caller pinned with kgs_host_register are DMA'd in place ("all"); a mix of pinned
+    and pageable inputs ("some") takes the staging path. Same bytes as the C restatement either way,
+    and the Montgomery write-back is unchanged."""
+    from oracle import cbackend as C
+    nbits, npols = 13, 2  # 256 KiB vectors: each its own pages (registration is page-granular)
+    path = f"/tmp/kgs_test_gpu_p{nbits}.ptau"
+    ctx = K.Context(0)
+    if not os.path.exists(path):
+        ctx.write_synthetic_ptau(path, nbits, common.tau())
+    ctx.load_ptau(path, nbits)
+    Fs, Ts, sF, sT = common.make_inputs(77, nbits, npols, True)
+    bufs = [bytearray(x) for x in Fs + Ts + [sF, sT]]
+    pinned = bufs if which == "all" else bufs[::2]
+    handles = [K.host_register(b) for b in pinned]
+    try:
+        bF, bT = bufs[:npols], bufs[npols:2 * npols]
+        coms, evs, mf, mt = ctx.prove(K.GRANDSUM, nbits, bF, bT, bufs[-2], bufs[-1])
+        coms2, evs2, mf2, mt2 = ctx.prove(K.GRANDSUM, nbits, Fs, Ts, sF, sT)
+    finally:
+        for h in handles:
+            K.host_unregister(h)
+    _, srs = C.load_srs_bytes(path)
+    ecoms, eevs = C.prove_raw(K.GRANDSUM, nbits, Fs, Ts, sF, sT, srs, 0)
+    assert coms == ecoms and evs == eevs
+    assert coms2 == ecoms and evs2 == eevs
+    assert mf == mf2 and mt == mt2
+    assert [bytes(b) for b in bufs] == Fs + Ts + [sF, sT]  # inputs untouched
+    ctx.close()
+
+
 def _sharded_run(K, world, ptau, nbits, kind, Fs, Ts, sF, sT):
     """`world` contexts (one per simulated rank, all on cuda:0), one host thread each, MSMs
     point-range sharded through an in-process all-gather. Returns every rank's proof."""
