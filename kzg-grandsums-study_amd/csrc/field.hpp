@@ -190,6 +190,95 @@ struct Fe {
     return r;
   }
 
+  // Two independent products with their instruction streams interleaved: every asm block carries
+  // the same two column terms of BOTH products (mad A, mad B, addc A, addc B, ...), so the serial
+  // accumulator chain of one product issues between the links of the other. A single product is one
+  // dependent chain (each mad reads the previous mad's 64-bit sum); at the 2 waves per SIMD of the
+  // NTT passes that chain, not the issue rate, set the pace.
+  __device__ __forceinline__ static void mac_x2(uint64_t& accA, uint32_t& tA, uint32_t xA, uint32_t yA, uint64_t& accB,
+                                                uint32_t& tB, uint32_t xB, uint32_t yB) {
+    uint64_t cA, cB;
+    asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\tv_mad_u64_u32 %2, %5, %8, %9, %2\n\t"
+        "v_addc_co_u32 %1, %4, 0, %1, %4\n\tv_addc_co_u32 %3, %5, 0, %3, %5"
+        : "+v"(accA), "+v"(tA), "+v"(accB), "+v"(tB), "=&s"(cA), "=&s"(cB)
+        : "v"(xA), "v"(yA), "v"(xB), "v"(yB));
+  }
+  __device__ __forceinline__ static void mac_x2_init(uint64_t& accA, uint32_t& tA, uint32_t xA, uint32_t yA,
+                                                     uint64_t& accB, uint32_t& tB, uint32_t xB, uint32_t yB) {
+    uint64_t cA, cB;
+    asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\tv_mad_u64_u32 %2, %5, %8, %9, %2\n\t"
+        "v_addc_co_u32 %1, %4, 0, 0, %4\n\tv_addc_co_u32 %3, %5, 0, 0, %5"
+        : "+v"(accA), "=&v"(tA), "+v"(accB), "=&v"(tB), "=&s"(cA), "=&s"(cB)
+        : "v"(xA), "v"(yA), "v"(xB), "v"(yB));
+  }
+  // two terms of one column of each product (a_j b_k and m_j p_k of A, the same of B)
+  __device__ __forceinline__ static void mac2_x2(uint64_t& accA, uint32_t& tA, uint32_t xA0, uint32_t yA0, uint32_t xA1,
+                                                 uint32_t yA1, uint64_t& accB, uint32_t& tB, uint32_t xB0, uint32_t yB0,
+                                                 uint32_t xB1, uint32_t yB1) {
+    uint64_t cA0, cB0, cA1, cB1;
+    asm("v_mad_u64_u32 %0, %4, %8, %9, %0\n\tv_mad_u64_u32 %2, %5, %12, %13, %2\n\t"
+        "v_addc_co_u32 %1, %4, 0, %1, %4\n\tv_addc_co_u32 %3, %5, 0, %3, %5\n\t"
+        "v_mad_u64_u32 %0, %6, %10, %11, %0\n\tv_mad_u64_u32 %2, %7, %14, %15, %2\n\t"
+        "v_addc_co_u32 %1, %6, 0, %1, %6\n\tv_addc_co_u32 %3, %7, 0, %3, %7"
+        : "+v"(accA), "+v"(tA), "+v"(accB), "+v"(tB), "=&s"(cA0), "=&s"(cB0), "=&s"(cA1), "=&s"(cB1)
+        : "v"(xA0), "v"(yA0), "v"(xA1), "v"(yA1), "v"(xB0), "v"(yB0), "v"(xB1), "v"(yB1));
+  }
+  __device__ __forceinline__ static void mac2_x2_init(uint64_t& accA, uint32_t& tA, uint32_t xA0, uint32_t yA0,
+                                                      uint32_t xA1, uint32_t yA1, uint64_t& accB, uint32_t& tB,
+                                                      uint32_t xB0, uint32_t yB0, uint32_t xB1, uint32_t yB1) {
+    uint64_t cA0, cB0, cA1, cB1;
+    asm("v_mad_u64_u32 %0, %4, %8, %9, %0\n\tv_mad_u64_u32 %2, %5, %12, %13, %2\n\t"
+        "v_addc_co_u32 %1, %4, 0, 0, %4\n\tv_addc_co_u32 %3, %5, 0, 0, %5\n\t"
+        "v_mad_u64_u32 %0, %6, %10, %11, %0\n\tv_mad_u64_u32 %2, %7, %14, %15, %2\n\t"
+        "v_addc_co_u32 %1, %6, 0, %1, %6\n\tv_addc_co_u32 %3, %7, 0, %3, %7"
+        : "+v"(accA), "=&v"(tA), "+v"(accB), "=&v"(tB), "=&s"(cA0), "=&s"(cB0), "=&s"(cA1), "=&s"(cB1)
+        : "v"(xA0), "v"(yA0), "v"(xA1), "v"(yA1), "v"(xB0), "v"(yB0), "v"(xB1), "v"(yB1));
+  }
+  // RA = A*B*R^-1, RB = C*D*R^-1, each in [0, 2p) for inputs in [0, 2p): mul_nored twice, interleaved.
+  // The outputs must not alias the inputs (mul_nored_x2_ip for X *= B, Y *= D).
+  __device__ __forceinline__ static void mul_nored_x2(const Fe& A, const Fe& B, const Fe& C, const Fe& D, Fe& RA,
+                                                      Fe& RB) {
+    const uint32_t *a = A.v, *b = B.v, *c = C.v, *d = D.v;
+    uint32_t m[8], n[8];
+    uint64_t acc = 0, acd = 0;
+    uint32_t ta, tc;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      if (i == 0) {
+        mac_x2_init(acc, ta, a[0], b[0], acd, tc, c[0], d[0]);
+      } else {
+        mac2_x2_init(acc, ta, a[0], b[i], m[0], P::p[i], acd, tc, c[0], d[i], n[0], P::p[i]);
+#pragma unroll
+        for (int j = 1; j < i; j++)
+          mac2_x2(acc, ta, a[j], b[i - j], m[j], P::p[i - j], acd, tc, c[j], d[i - j], n[j], P::p[i - j]);
+        mac_x2(acc, ta, a[i], b[0], acd, tc, c[i], d[0]);
+      }
+      m[i] = (uint32_t)acc * P::inv;
+      n[i] = (uint32_t)acd * P::inv;
+      mac_x2(acc, ta, m[i], P::p[0], acd, tc, n[i], P::p[0]);
+      acc = (acc >> 32) | ((uint64_t)ta << 32);
+      acd = (acd >> 32) | ((uint64_t)tc << 32);
+    }
+#pragma unroll
+    for (int i = 8; i < 15; i++) {
+      mac2_x2_init(acc, ta, a[i - 7], b[7], m[i - 7], P::p[7], acd, tc, c[i - 7], d[7], n[i - 7], P::p[7]);
+#pragma unroll
+      for (int j = i - 6; j < 8; j++)
+        mac2_x2(acc, ta, a[j], b[i - j], m[j], P::p[i - j], acd, tc, c[j], d[i - j], n[j], P::p[i - j]);
+      RA.v[i - 8] = (uint32_t)acc;
+      RB.v[i - 8] = (uint32_t)acd;
+      acc = (acc >> 32) | ((uint64_t)ta << 32);
+      acd = (acd >> 32) | ((uint64_t)tc << 32);
+    }
+    RA.v[7] = (uint32_t)acc;
+    RB.v[7] = (uint32_t)acd;
+  }
+
+  __device__ __forceinline__ static void mul_nored_x2_ip(Fe& X, const Fe& B, Fe& Y, const Fe& D) {
+    const Fe a = X, c = Y;
+    mul_nored_x2(a, B, c, D, X, Y);
+  }
+
   __device__ __forceinline__ friend Fe operator*(const Fe& A, const Fe& B) { return reduce_once(mul_nored(A, B)); }
 
   __device__ __forceinline__ Fe sqr() const { return (*this) * (*this); }

@@ -18,6 +18,7 @@
 // entries for the largest domain M), so the butterflies of one stage read consecutive twiddles
 // (coalesced: consecutive lanes have consecutive t) instead of a strided walk through w_M^j.
 #include <algorithm>
+#include <cstdlib>
 
 #include "kernels.hpp"
 
@@ -205,13 +206,21 @@ __device__ __forceinline__ void lds_map(uint32_t e, int K, int logd, int lblog, 
   }
 }
 
-__device__ __forceinline__ uint64_t lds_idx(uint64_t col, uint32_t j, int K, int logd) {
-  const uint64_t lo = col & ((1ull << logd) - 1), hi = col >> logd;
-  return (hi << (logd + K)) | ((uint64_t)j << logd) | lo;
+// element indices < 2^28 (logm <= 28): 32-bit index arithmetic
+__device__ __forceinline__ uint32_t lds_idx(uint32_t col, uint32_t j, int K, int logd) {
+  const uint32_t lo = col & ((1u << logd) - 1), hi = col >> logd;
+  return (hi << (logd + K)) | (j << logd) | lo;
 }
 
 #ifndef KGS_NTT_LDS_AOS
+// 16-byte slot e of a plane -> swizzled slot: the low 4 bits (the slot's bank group within a 256-byte
+// LDS row) XORed with bits 4-7 and 8-11, a bijection on the tile. The contiguous pass's address-order
+// staging (lanes step j, slot stride LB) and its rounds hit 2-6 slots per bank group in each 16-lane
+// phase of a ds_read/write_b128 without it (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.54); with it every
+// access pattern of every pass plan is at most 2-way (profiles/r03/ntt_lds_swizzle.txt).
+__device__ __forceinline__ uint32_t lds_swz(uint32_t e) { return e ^ ((e >> 4) & 15u) ^ ((e >> 8) & 15u); }
 __device__ __forceinline__ fr lds_ld(const uint32_t* lds, uint32_t e) {
+  e = lds_swz(e);
   const uint4 a = reinterpret_cast<const uint4*>(lds)[e];
   const uint4 b = reinterpret_cast<const uint4*>(lds + 4 * LDS_ELEMS)[e];
   fr r;
@@ -220,6 +229,7 @@ __device__ __forceinline__ fr lds_ld(const uint32_t* lds, uint32_t e) {
   return r;
 }
 __device__ __forceinline__ void lds_st(uint32_t* lds, uint32_t e, const fr& x) {
+  e = lds_swz(e);
   reinterpret_cast<uint4*>(lds)[e] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
   reinterpret_cast<uint4*>(lds + 4 * LDS_ELEMS)[e] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
 }
@@ -228,120 +238,266 @@ __device__ __forceinline__ fr lds_ld(const uint32_t* lds, uint32_t e) { return f
 __device__ __forceinline__ void lds_st(uint32_t* lds, uint32_t e, const fr& x) { x.store(lds + 8 * e); }
 #endif
 
+// Where a round's elements come from / go to: the LDS tile, or global memory directly (the pass's
+// first round reads its elements from HBM into registers and its last round writes them back from
+// registers, with no LDS staging round trip and no barrier around them). Direct access is coalesced
+// when a tile's columns are runs of LB >= 4 consecutive elements (group stride d >= LB): consecutive
+// lanes then hold consecutive elements. The pass whose columns are contiguous blocks (d < LB: the
+// DIF-last / DIT-first pass) stages through LDS in address order instead.
+struct ntt_io {
+  uint32_t* data;
+  const uint32_t* in;   // first pass: source (DIF: zero beyond in_len, times pre[idx]; DIT: bit reversal)
+  uint64_t in_len;
+  int in_bitrev;
+  const uint32_t* pre;
+  const uint32_t* post;  // last pass: times post[idx] and / or the scalar *post_s
+  const uint32_t* post_s;
+  int logm;
+};
+
+template <bool DIT>
+__device__ __forceinline__ fr ntt_load(const ntt_io& io, uint64_t idx) {
+  if (!io.in) return fr::load(io.data + 8 * idx);
+  if (DIT) return fr::load(io.in + 8 * (io.in_bitrev ? idx : (uint64_t)bitrev((uint32_t)idx, io.logm)));
+  if (idx >= io.in_len) return fr::zero();
+  fr x = fr::load(io.in + 8 * idx);
+  if (io.pre) x = x * fr::load(io.pre + 8 * idx);
+  return x;
+}
+__device__ __forceinline__ void ntt_store(const ntt_io& io, uint64_t idx, fr y) {
+  if (io.post) y = y * fr::load(io.post + 8 * idx);
+  if (io.post_s) y = y * fr::load(io.post_s);
+  canon_out(y).store(io.data + 8 * idx);
+}
+
+// butterfly groups of lds_round: (r, r + dist) for the given register indices
+__device__ __forceinline__ void bfly_pair_triv(fr* x, int r0, int r1, int dist) {  // w = 1 for both
+  const fr a0 = x[r0], b0 = x[r0 + dist], a1 = x[r1], b1 = x[r1 + dist];
+  x[r0] = fr::add_lazy(a0, b0);
+  x[r0 + dist] = fr::sub_lazy(a0, b0);
+  x[r1] = fr::add_lazy(a1, b1);
+  x[r1 + dist] = fr::sub_lazy(a1, b1);
+}
+template <bool DIT>
+__device__ __forceinline__ void bfly_pair_x2(fr* x, int r0, int r1, int dist, const uint32_t* w0, const uint32_t* w1) {
+  if (DIT) {
+    fr b0, b1;
+    fr::mul_nored_x2(x[r0 + dist], fr::load(w0), x[r1 + dist], fr::load(w1), b0, b1);
+    const fr a0 = x[r0], a1 = x[r1];
+    x[r0] = fr::add_lazy(a0, b0);
+    x[r0 + dist] = fr::sub_lazy(a0, b0);
+    x[r1] = fr::add_lazy(a1, b1);
+    x[r1 + dist] = fr::sub_lazy(a1, b1);
+  } else {
+    const fr d0 = fr::sub_2p(x[r0], x[r0 + dist]), d1 = fr::sub_2p(x[r1], x[r1 + dist]);
+    x[r0] = fr::add_lazy(x[r0], x[r0 + dist]);
+    x[r1] = fr::add_lazy(x[r1], x[r1 + dist]);
+    fr::mul_nored_x2(d0, fr::load(w0), d1, fr::load(w1), x[r0 + dist], x[r1 + dist]);
+  }
+}
 // one register round of R stages of a pass on the 2^R elements j = jb + js * r (r < 2^R) of column
 // col: stage k of the round is pass stage kp0 + k; DIF pairs (r, r + 2^(R-1-k)), DIT (r, r + 2^k)
-template <int R, bool DIT>
-__device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restrict__ tw, uint32_t cl, uint64_t col,
-                                          uint32_t jb, uint32_t js, int K, int logd, int lb, int kp0) {
+template <int R, bool DIT, bool GIN, bool GOUT>
+__device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restrict__ tw, const ntt_io& io, uint32_t cl,
+                                          uint32_t col, uint32_t jb, uint32_t js, int K, int logd, int lb, int kp0) {
   fr x[1 << R];
+  if (GIN && !DIT && io.in && io.pre && R >= 2) {
+    // first DIF pass with a coset pre-scaling: the products two at a time
 #pragma unroll
-  for (int r = 0; r < (1 << R); r++) x[r] = lds_ld(lds, (jb + js * r) * lb + cl);
+    for (int r = 0; r < (1 << R); r += 2) {
+      const uint32_t i0 = lds_idx(col, jb + js * r, K, logd), i1 = lds_idx(col, jb + js * (r + 1), K, logd);
+      const fr a0 = i0 < io.in_len ? fr::load(io.in + 8 * i0) : fr::zero();
+      const fr a1 = i1 < io.in_len ? fr::load(io.in + 8 * i1) : fr::zero();
+      fr::mul_nored_x2(a0, fr::load(io.pre + 8 * i0), a1, fr::load(io.pre + 8 * i1), x[r], x[r + 1]);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < (1 << R); r++)
+      x[r] = GIN ? ntt_load<DIT>(io, lds_idx(col, jb + js * r, K, logd)) : lds_ld(lds, (jb + js * r) * lb + cl);
+  }
 #pragma unroll
   for (int k = 0; k < R; k++) {
     const int kp = kp0 + k;                                 // stage within the pass
     const int logh = DIT ? logd + kp : logd + K - 1 - kp;   // half-distance h = 2^logh
     const int dist = DIT ? 1 << k : 1 << (R - 1 - k);       // register distance
+#ifndef KGS_NTT_SINGLE
+    if constexpr (R >= 2) {
+      // Butterflies two at a time (q, q + half), their products interleaved (fr::mul_nored_x2; four at a
+      // time, fr::mul_nored_x4 at 232 VGPRs, measured 1.25x slower: profiles/r03/ntt_x2_x4.txt). A pair
+      // whose twiddles are all w^0 = 1 across the wave (low stages of the contiguous pass, where t depends
+      // on the register index only) skips its products; otherwise a lane with t == 0 multiplies by
+      // tw[h] = 1 (a product in [0, 2p) congruent to its input: same canonical output).
+      constexpr int half = 1 << (R - 2);
+      const uint32_t hm = (1u << logh) - 1;
+#define KGS_RR(q) ((((q) / dist) * 2 * dist) + ((q) % dist))
+#define KGS_T(q) (lds_idx(col, jb + js * KGS_RR(q), K, logd) & hm)
+      {
 #pragma unroll
-    for (int q = 0; q < (1 << (R - 1)); q++) {
-      const int r = ((q / dist) * 2 * dist) + (q % dist);
-      const uint64_t idx = lds_idx(col, jb + js * r, K, logd);
-      const uint64_t t = idx & ((1ull << logh) - 1);
-      const uint32_t* w = tw + 8 * ((1ull << logh) + t);  // stage table: w_{2h}^t = tw[h + t]
-      if (DIT)
-        bfly_dit(x[r], x[r + dist], w, t != 0);
-      else
-        bfly_dif(x[r], x[r + dist], w, t != 0);
+        for (int qa = 0; qa < half; qa++) {
+          const uint32_t t0 = KGS_T(qa), t1 = KGS_T(qa + half);
+          if (__all(t0 == 0 && t1 == 0))
+            bfly_pair_triv(x, KGS_RR(qa), KGS_RR(qa + half), dist);
+          else
+            bfly_pair_x2<DIT>(x, KGS_RR(qa), KGS_RR(qa + half), dist, tw + 8 * (hm + 1 + t0), tw + 8 * (hm + 1 + t1));
+        }
+      }
+#undef KGS_T
+#undef KGS_RR
+    } else
+#endif
+    {
+#pragma unroll
+      for (int q = 0; q < (1 << (R - 1)); q++) {
+        const int r = ((q / dist) * 2 * dist) + (q % dist);
+        const uint32_t idx = lds_idx(col, jb + js * r, K, logd);
+        const uint32_t t = idx & ((1u << logh) - 1);
+        const uint32_t* w = tw + 8 * ((1u << logh) + t);  // stage table: w_{2h}^t = tw[h + t]
+        if (DIT)
+          bfly_dit(x[r], x[r + dist], w, t != 0);
+        else
+          bfly_dif(x[r], x[r + dist], w, t != 0);
+      }
     }
   }
+  if (GOUT && R >= 2) {
+    // last pass: the post-scalings two products at a time, then canonical stores
+    if (io.post) {
 #pragma unroll
-  for (int r = 0; r < (1 << R); r++) lds_st(lds, (jb + js * r) * lb + cl, x[r]);
+      for (int r = 0; r < (1 << R); r += 2) {
+        const uint32_t i0 = lds_idx(col, jb + js * r, K, logd), i1 = lds_idx(col, jb + js * (r + 1), K, logd);
+        fr::mul_nored_x2_ip(x[r], fr::load(io.post + 8 * i0), x[r + 1], fr::load(io.post + 8 * i1));
+      }
+    }
+    if (io.post_s) {
+      const fr ps = fr::load(io.post_s);
+#pragma unroll
+      for (int r = 0; r < (1 << R); r += 2) fr::mul_nored_x2_ip(x[r], ps, x[r + 1], ps);
+    }
+#pragma unroll
+    for (int r = 0; r < (1 << R); r++) canon_out(x[r]).store(io.data + 8 * lds_idx(col, jb + js * r, K, logd));
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < (1 << R); r++) {
+    if (GOUT)
+      ntt_store(io, lds_idx(col, jb + js * r, K, logd), x[r]);
+    else
+      lds_st(lds, (jb + js * r) * lb + cl, x[r]);
+  }
 }
 
-// K1 + K2 stages from s0. in: first-pass source (DIF: zero beyond in_len, times pre[idx]; DIT: gathered
-// through bit reversal unless in_bitrev); post / post_s: last-pass multipliers (DIT).
-template <int K1, int K2, bool DIT>
-__global__ void __launch_bounds__(LDS_NT) k_ntt_lds_pass(uint32_t* __restrict__ data, const uint32_t* __restrict__ in,
-                                                      uint64_t in_len, int in_bitrev, const uint32_t* __restrict__ pre,
-                                                      const uint32_t* __restrict__ tw, int logm, int s0,
-                                                      const uint32_t* __restrict__ post,
-                                                      const uint32_t* __restrict__ post_s) {
+// all groups of one round of a pass: the round covers the j-bits [b0, b0 + R) of every column of the
+// tile (a thread holds the 2^R elements that differ in those bits, the other K - R bits fixed).
+// DIF rounds run from the top j-bits down, DIT rounds from bit 0 up; kp0 = the round's first stage
+// within the pass.
+template <int R, bool DIT, bool GIN, bool GOUT>
+__device__ __forceinline__ void lds_round_all(uint32_t* lds, const uint32_t* __restrict__ tw, const ntt_io& io,
+                                              uint32_t col0, int K, int logd, int lblog, int b0) {
+  const int kp0 = DIT ? b0 : K - b0 - R;
+  for (uint32_t g = threadIdx.x; g < (LDS_ELEMS >> R); g += LDS_NT) {
+    const uint32_t cl = g & ((1u << lblog) - 1), jq = g >> lblog;
+    const uint32_t jb = (jq & ((1u << b0) - 1)) | ((jq >> b0) << (b0 + R));
+    lds_round<R, DIT, GIN, GOUT>(lds, tw, io, cl, col0 + cl, jb, 1u << b0, K, logd, 1 << lblog, kp0);
+  }
+}
+
+// K1 + K2 + K3 stages from s0 (two or three register rounds with an LDS exchange between rounds).
+// DIRECT: the first round loads from and the last round stores to global memory (d >= LB); else the
+// tile is loaded into / stored from LDS in address order around the rounds.
+template <int K1, int K2, int K3, bool DIT, bool DIRECT>
+__global__ void __launch_bounds__(LDS_NT) k_ntt_lds_pass(ntt_io io, const uint32_t* __restrict__ tw, int s0) {
   KGS_AUX_PRIO();
-  constexpr int K = K1 + K2;
+  constexpr int K = K1 + K2 + K3;
   constexpr int LBLOG = NTT_ELOG - K;
   constexpr int LB = 1 << LBLOG;
   __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_ELEMS * 8];
-  const int logd = DIT ? s0 : logm - s0 - K;
-  const uint64_t col0 = (uint64_t)blockIdx.x * LB;
-  // load (address order)
-  for (uint32_t e = threadIdx.x; e < LDS_ELEMS; e += LDS_NT) {
-    uint32_t j, cl;
-    lds_map(e, K, logd, LBLOG, j, cl);
-    const uint64_t idx = lds_idx(col0 + cl, j, K, logd);
-    fr x;
-    if (in) {
-      if (DIT) {
-        x = fr::load(in + 8 * (in_bitrev ? idx : (uint64_t)bitrev((uint32_t)idx, logm)));
-      } else if (idx < in_len) {
-        x = fr::load(in + 8 * idx);
-        if (pre) x = x * fr::load(pre + 8 * idx);
-      } else {
-        x = fr::zero();
-      }
-    } else {
-      x = fr::load(data + 8 * idx);
+  const int logd = DIT ? s0 : io.logm - s0 - K;
+  const uint32_t col0 = blockIdx.x * LB;
+  if (!DIRECT) {  // load (address order)
+    for (uint32_t e = threadIdx.x; e < LDS_ELEMS; e += LDS_NT) {
+      uint32_t j, cl;
+      lds_map(e, K, logd, LBLOG, j, cl);
+      lds_st(lds, j * LB + cl, ntt_load<DIT>(io, lds_idx(col0 + cl, j, K, logd)));
     }
-    lds_st(lds, j * LB + cl, x);
+    __syncthreads();
   }
+  // DIF: bits [K-K1, K), [K-K1-K2, K-K1), [0, K3); DIT: [0, K1), [K1, K1+K2), [K1+K2, K)
+  lds_round_all<K1, DIT, DIRECT, false>(lds, tw, io, col0, K, logd, LBLOG, DIT ? 0 : K - K1);
   __syncthreads();
-  // round 1: DIF pairs at j-distances 2^(K-1) .. 2^K2 (j = jl + 2^K2 r); DIT 1 .. 2^(K1-1) (j = 2^K1 jh + r)
-  for (uint32_t g = threadIdx.x; g < (LDS_ELEMS >> K1); g += LDS_NT) {
-    const uint32_t cl = g & (LB - 1), jq = g >> LBLOG;
-    if (DIT)
-      lds_round<K1, true>(lds, tw, cl, col0 + cl, jq << K1, 1, K, logd, LB, 0);
-    else
-      lds_round<K1, false>(lds, tw, cl, col0 + cl, jq, 1u << K2, K, logd, LB, 0);
+  if constexpr (K3 > 0) {
+    lds_round_all<K2, DIT, false, false>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 : K3);
+    __syncthreads();
+    lds_round_all<K3, DIT, false, DIRECT>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 + K2 : 0);
+  } else {
+    lds_round_all<K2, DIT, false, DIRECT>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 : 0);
   }
-  __syncthreads();
-  // round 2: DIF j-distances 2^(K2-1) .. 1 (j = 2^K2 jh + r); DIT 2^K1 .. 2^(K-1) (j = jl + 2^K1 r)
-  for (uint32_t g = threadIdx.x; g < (LDS_ELEMS >> K2); g += LDS_NT) {
-    const uint32_t cl = g & (LB - 1), jq = g >> LBLOG;
-    if (DIT)
-      lds_round<K2, true>(lds, tw, cl, col0 + cl, jq, 1u << K1, K, logd, LB, K1);
-    else
-      lds_round<K2, false>(lds, tw, cl, col0 + cl, jq << K2, 1, K, logd, LB, K1);
-  }
-  __syncthreads();
-  fr ps;
-  if (post_s) ps = fr::load(post_s);
-  for (uint32_t e = threadIdx.x; e < LDS_ELEMS; e += LDS_NT) {
-    uint32_t j, cl;
-    lds_map(e, K, logd, LBLOG, j, cl);
-    const uint64_t idx = lds_idx(col0 + cl, j, K, logd);
-    fr y = lds_ld(lds, j * LB + cl);
-    if (post) y = y * fr::load(post + 8 * idx);
-    if (post_s) y = y * ps;
-    canon_out(y).store(data + 8 * idx);
+  if (!DIRECT) {  // store (address order)
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < LDS_ELEMS; e += LDS_NT) {
+      uint32_t j, cl;
+      lds_map(e, K, logd, LBLOG, j, cl);
+      ntt_store(io, lds_idx(col0 + cl, j, K, logd), lds_ld(lds, j * LB + cl));
+    }
   }
 }
 
 #ifndef KGS_NO_NTT_LDS
-// stages per pass for m = 2^logm: LDS passes of up to 6 stages while >= 4 remain, radix-8/4/2 after
-static inline int lds_pass_stages(int left) { return left >= 6 ? 6 : left >= 4 ? left : 0; }
 // LDS passes need m >= the tile (2^NTT_ELOG elements)
 constexpr int LDS_MIN_LOGM = NTT_ELOG > 11 ? NTT_ELOG : 11;
+constexpr int LDS_MAX_K = NTT_ELOG - 2 < 9 ? NTT_ELOG - 2 : 9;  // >= 4 columns (128 B runs) per tile
+
+// Pass plan of an m = 2^logm transform (logm >= LDS_MIN_LOGM), in DIF order: ceil(logm / 9) LDS passes
+// of 4..9 stages; the pass whose columns are contiguous (DIF last / DIT first: group stride 1) takes up
+// to 9 stages (three register rounds), the others 6 (two rounds, 1 KiB runs) unless more are needed.
+// 2^20 = 6+6+8, 2^21 = 6+6+9, 2^22 = 7+6+9, 2^24 = 8+7+9: three passes where the radix-8 tail pass
+// made four.
+static int lds_plan(int logm, int* ks) {
+  const int P = (logm + LDS_MAX_K - 1) / LDS_MAX_K;
+  int E = logm - 6 * (P - 1);
+  if (E > LDS_MAX_K) E = LDS_MAX_K;
+  int rest = logm - E;
+  for (int i = 0; i < P - 1; i++) {
+    const int left = P - 1 - i;
+    ks[i] = (rest + left - 1) / left;
+    rest -= ks[i];
+  }
+  ks[P - 1] = E;
+  return P;
+}
 
 static void launch_lds_pass(hipStream_t st, int K, bool dit, uint32_t* data, const uint32_t* in, uint64_t in_len,
                             int in_bitrev, const uint32_t* pre, const uint32_t* tw, int logm, int s0,
                             const uint32_t* post, const uint32_t* post_s) {
   const unsigned blocks = (unsigned)((1ull << logm) / LDS_ELEMS);
-#define KGS_LDS_LAUNCH(A, B, D)                                                                                  \
-  hipLaunchKernelGGL((k_ntt_lds_pass<A, B, D>), dim3(blocks), dim3(LDS_NT), 0, st, data, in, in_len, in_bitrev, pre, \
-                     tw, logm, s0, post, post_s)
-  if (dit) {
-    if (K == 6) KGS_LDS_LAUNCH(3, 3, true); else if (K == 5) KGS_LDS_LAUNCH(3, 2, true); else KGS_LDS_LAUNCH(2, 2, true);
-  } else {
-    if (K == 6) KGS_LDS_LAUNCH(3, 3, false); else if (K == 5) KGS_LDS_LAUNCH(3, 2, false); else KGS_LDS_LAUNCH(2, 2, false);
+  const ntt_io io{data, in, in_len, in_bitrev, pre, post, post_s, logm};
+  const int logd = dit ? s0 : logm - s0 - K;
+  static const bool staged = getenv("KGS_NTT_STAGED") != nullptr;  // A/B: every pass staged through LDS
+  const bool direct = logd >= NTT_ELOG - K && !staged;
+#define KGS_LDS_LAUNCH(A, B, C, D, E) \
+  hipLaunchKernelGGL((k_ntt_lds_pass<A, B, C, D, E>), dim3(blocks), dim3(LDS_NT), 0, st, io, tw, s0)
+#define KGS_LDS_BY_K(D, E)                          \
+  switch (K) {                                      \
+    case 9: KGS_LDS_LAUNCH(3, 3, 3, D, E); break;   \
+    case 8: KGS_LDS_LAUNCH(3, 3, 2, D, E); break;   \
+    case 7: KGS_LDS_LAUNCH(3, 2, 2, D, E); break;   \
+    case 6: KGS_LDS_LAUNCH(3, 3, 0, D, E); break;   \
+    case 5: KGS_LDS_LAUNCH(3, 2, 0, D, E); break;   \
+    default: KGS_LDS_LAUNCH(2, 2, 0, D, E); break;  \
   }
+  if (dit) {
+    if (direct) {
+      KGS_LDS_BY_K(true, true)
+    } else {
+      KGS_LDS_BY_K(true, false)
+    }
+  } else {
+    if (direct) {
+      KGS_LDS_BY_K(false, true)
+    } else {
+      KGS_LDS_BY_K(false, false)
+    }
+  }
+#undef KGS_LDS_BY_K
 #undef KGS_LDS_LAUNCH
 }
 #endif
@@ -356,20 +512,21 @@ void ntt_dif(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t in_len,
     }
     return;
   }
+#ifndef KGS_NO_NTT_LDS
+  if (logm >= LDS_MIN_LOGM) {
+    int ks[8];
+    const int P = lds_plan(logm, ks);
+    for (int i = 0, s0 = 0; i < P; s0 += ks[i++])
+      launch_lds_pass(st, ks[i], false, out, i ? nullptr : in, in_len, 1, i ? nullptr : pre, tw, logm, s0, nullptr,
+                      nullptr);
+    return;
+  }
+#endif
   int s0 = 0;
   bool first = true;
   while (s0 < logm) {
     const uint32_t* src = first ? in : nullptr;
     const uint32_t* p = first ? pre : nullptr;
-#ifndef KGS_NO_NTT_LDS
-    const int KL = logm >= LDS_MIN_LOGM ? lds_pass_stages(logm - s0) : 0;
-    if (KL) {
-      launch_lds_pass(st, KL, false, out, src, in_len, 1, p, tw, logm, s0, nullptr, nullptr);
-      s0 += KL;
-      first = false;
-      continue;
-    }
-#endif
     int K = logm - s0 >= 3 ? 3 : logm - s0;
     uint64_t groups = (1ull << logm) >> K;
     if (K == 3)
@@ -389,25 +546,27 @@ void ntt_dit(hipStream_t st, uint32_t* out, const uint32_t* in, int in_bitrev, i
     launch_scale_copy(st, out, in, 1, post, post_s);
     return;
   }
-  // passes: LDS passes of up to 6 stages while >= 4 stages remain (m >= 2048), then radix-8/4/2
-  // passes; otherwise the first pass handles the remainder so the last pass is a full radix-8 one
+#ifndef KGS_NO_NTT_LDS
+  // m >= 2^11: the LDS passes of lds_plan in reverse (the contiguous, up-to-9-stage pass first)
+  if (logm >= LDS_MIN_LOGM) {
+    int ks[8];
+    const int P = lds_plan(logm, ks);
+    for (int i = 0, s0 = 0; i < P; i++) {
+      const int K = ks[P - 1 - i];
+      const bool last = i == P - 1;
+      launch_lds_pass(st, K, true, out, i ? nullptr : in, 0, in_bitrev, nullptr, tw, logm, s0, last ? post : nullptr,
+                      last ? post_s : nullptr);
+      s0 += K;
+    }
+    return;
+  }
+#endif
+  // radix-8/4/2 passes; the first pass handles the remainder so the last pass is a full radix-8 one
   int rem = logm % 3;
   int s0 = 0;
   bool first = true;
   while (s0 < logm) {
     const uint32_t* src = first ? in : nullptr;
-#ifndef KGS_NO_NTT_LDS
-    const int KL = logm >= LDS_MIN_LOGM ? lds_pass_stages(logm - s0) : 0;
-    if (KL) {
-      const bool last = s0 + KL == logm;
-      launch_lds_pass(st, KL, true, out, src, 0, in_bitrev, nullptr, tw, logm, s0, last ? post : nullptr,
-                      last ? post_s : nullptr);
-      s0 += KL;
-      first = false;
-      continue;
-    }
-    if (logm >= LDS_MIN_LOGM) rem = 0;
-#endif
     int K = first && rem ? rem : 3;
     if (K > logm - s0) K = logm - s0;
     uint64_t groups = (1ull << logm) >> K;

@@ -1436,8 +1436,9 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   for (size_t v = 0; direct && v < in_jobs.size(); v++) direct = pins.pin(in_jobs[v].src, E);
   if (!direct) pins.release_from(0);
   if (direct) {
-    // zero-copy: every input DMA'd straight from the caller's (now pinned) buffer; vector 0 on the
-    // main stream, the others on the copy stream with the event their first kernel waits for
+    // zero-copy: every input DMA'd straight from the caller's pinned buffer, one after the other on the
+    // copy stream (not two streams at once: F_0 then arrives after one vector's transfer time instead
+    // of sharing the link with T_0), each with the event its first kernel waits for
     if (!ctx->st_copy) {
       HC(hipStreamCreateWithFlags(&ctx->st_copy, hipStreamNonBlocking));
       HC(hipEventCreateWithFlags(&ctx->ev_copy, hipEventDisableTiming));
@@ -1448,8 +1449,7 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
       ctx->ev_in.push_back(e);
     }
     in.ready.assign(in_jobs.size(), nullptr);
-    HC(hipMemcpyAsync(dsts[0], in_jobs[0].src, E, hipMemcpyHostToDevice, ctx->st));
-    for (size_t v = 1; v < in_jobs.size(); v++) {
+    for (size_t v = 0; v < in_jobs.size(); v++) {
       HC(hipMemcpyAsync(dsts[v], in_jobs[v].src, E, hipMemcpyHostToDevice, ctx->st_copy));
       HC(hipEventRecord(ctx->ev_in[v], ctx->st_copy));
       in.ready[v] = ctx->ev_in[v];

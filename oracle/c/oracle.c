@@ -705,6 +705,19 @@ int orc_max_threads(void) {
  * p(x) = (x^n - 1)/n * sum_i e_i w^i / (x - w^i) (barycentric; x not in <w_n>). Test checker for the
  * transcript-independent commitments of large proofs: C(F) == F(tau) G1 (tests/test_gpu_configs.py).
  * Chunked Montgomery batch inversion, one chunk per thread. */
+/* NTT of m = 2^k Montgomery elements in place, natural order in and out ([ffjs] Fr.fft / Fr.ifft,
+ * polynomial.js:34,373,392): the checker of the GPU transforms at sizes the Python oracle is too slow for */
+void orc_ntt(uint8_t* data_mont, uint64_t m, int inverse, int threads) {
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#endif
+  fe* a = (fe*)malloc(sizeof(fe) * (m ? m : 1));
+  memcpy(a, data_mont, 32 * m);
+  ntt(a, m, inverse);
+  memcpy(data_mont, a, 32 * m);
+  free(a);
+}
+
 int orc_eval_evals_std(const uint8_t* evals_std, int nbits, const uint8_t x_std[32], uint8_t out_std[32]) {
   const uint64_t n = 1ull << nbits;
   uint64_t xs[4];

@@ -30,6 +30,8 @@ def lib():
         L.orc_msm.restype = None
         L.orc_keccak256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
         L.orc_keccak256.restype = None
+        L.orc_ntt.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+        L.orc_ntt.restype = None
         L.orc_eval_evals_std.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p]
         _lib = L
     return _lib
@@ -42,6 +44,13 @@ def eval_evals_std(evals_std, nbits, x):
     if rc != 0:
         raise ValueError("x lies in the evaluation domain")
     return int.from_bytes(out.raw, "little")
+
+
+def ntt(data_mont, inverse=False, threads=0):
+    """Natural-order NTT / inverse NTT of Montgomery-form bytes (oracle.c ntt)."""
+    buf = ctypes.create_string_buffer(bytes(data_mont), len(data_mont))
+    lib().orc_ntt(buf, len(data_mont) // 32, 1 if inverse else 0, threads)
+    return buf.raw[:len(data_mont)]
 
 
 def load_srs_bytes(ptau_path):

@@ -84,6 +84,20 @@ def test_ntt(ctx9, logm):
     assert unmb(ctx9.ntt(common.mont_bytes(v), True)) == OP.ntt(v, True)
 
 
+# 18..22: three-pass plans with up to 9 stages in one pass (lds_plan: 9+9, 6+6+7, 6+6+8, 6+6+9, 7+6+9),
+# byte-for-byte against the C restatement's transform (oracle.c ntt)
+@pytest.mark.parametrize("logm", [18, 19, 20, 21, 22])
+def test_ntt_large_vs_c_oracle(ctx9, logm):
+    import numpy as np
+    from oracle import cbackend as C
+    rng = np.random.Generator(np.random.PCG64(logm))
+    w = rng.integers(0, 2**64 - 1, size=(1 << logm, 4), dtype=np.uint64, endpoint=True)
+    w[:, 3] &= np.uint64((1 << 60) - 1)  # < r: canonical Montgomery-form elements
+    x = w.tobytes()
+    for inverse in (False, True):
+        assert ctx9.ntt(x, inverse) == C.ntt(x, inverse), inverse
+
+
 def test_msm(ctx9):
     srs = P.SRS(common.oracle_ptau(9), common.tau())
     rnd = random.Random(2)

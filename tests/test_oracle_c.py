@@ -23,6 +23,16 @@ def test_keccak():
         assert out.raw == keccak256(m)
 
 
+@pytest.mark.parametrize("logm", [0, 1, 2, 5, 8, 10])
+def test_ntt_matches_python_oracle(logm):
+    """oracle.c's transform (the checker of the GPU NTT at 2^18..2^22) against poly.ntt."""
+    from oracle import poly as OP
+    rnd = random.Random(logm)
+    v = [rnd.randrange(bn.R) for _ in range(1 << logm)]
+    for inverse in (False, True):
+        assert C.ntt(common.mont_bytes(v), inverse) == common.mont_bytes(OP.ntt(v, inverse))
+
+
 def test_msm_closed_form():
     _, srs = C.load_srs_bytes(common.oracle_ptau(9))
     o = P.SRS(common.oracle_ptau(9), common.tau())
