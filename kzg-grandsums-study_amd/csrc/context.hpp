@@ -175,7 +175,7 @@ struct kgs_ctx {
   // bucket accumulation
   hipStream_t st2 = nullptr;
   hipStream_t st_copy = nullptr;  // Montgomery write-back of the host-buffer boundary
-  hipEvent_t ev_fork = nullptr, ev_copy = nullptr, ev_copy2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_copy = nullptr, ev_copy2 = nullptr, ev_join = nullptr;
   std::vector<hipEvent_t> ev_in;  // kgs_prove: one per input vector DMA'd on the copy stream
   MsmWork mw2;
   int msm_lanes = 2;  // kgs_ctx_set_msm_lanes
@@ -208,6 +208,7 @@ struct kgs_ctx {
     if (ev_fork) hipEventDestroy(ev_fork);
     if (ev_copy) hipEventDestroy(ev_copy);
     if (ev_copy2) hipEventDestroy(ev_copy2);
+    if (ev_join) hipEventDestroy(ev_join);
     for (hipEvent_t e : ev_in) hipEventDestroy(e);
     if (st_copy) hipStreamDestroy(st_copy);
     if (st2) hipStreamDestroy(st2);

@@ -281,29 +281,25 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
   }
 }
 
-// Pass 2: every partition p is cut into G_p chunks; (1) per-chunk LDS histograms of lo, (2) one
-// workgroup per partition scans them into per-(lo, chunk) global bases and writes the bucket
-// offsets, (3) every chunk counting-sorts its entries through LDS and writes runs.
-// G_p = clamp(ceil(size_p / SL_CHUNK), 1, SL_G): a chunk of a uniform partition fits ONE LDS tile,
-// so each of its buckets leaves as one run of ~SL_CHUNK / 256 entries (≈ 190 B at 2^20 points: whole
-// 128-byte lines, where the round-2 tiles of a 16-way split wrote ≈ 60-byte runs, 1.46× write
-// amplification); a skewed partition (all points in one bucket: a selector polynomial's equal
-// coefficients) is spread over up to SL_G workgroups. -DKGS_SL_FIXED16 restores the fixed 16-way
-// split with 4096-entry tiles (A/B).
+// Pass 2: every partition p is cut into G_p chunks; (1) per-chunk LDS histograms of lo, (2) every
+// chunk's workgroup derives its per-lo global bases from its partition's chunk histograms (a 256-wide
+// scan; the chunk-0 workgroup also writes the bucket offsets), counting-sorts its entries through LDS
+// and writes each bucket's run with consecutive lanes.
+// G_p = clamp(ceil(size_p / SL_CHUNK), 1, SL_G) and a chunk fits ONE LDS tile, so each bucket leaves
+// a chunk as one run of ~SL_CHUNK / 256 entries: ~240 B at 2^20 points (2^20 / 256 partitions x 15
+// windows = 61 K entries = 4 chunks of 15.4 K), write amplification ~1 + 32 B / run. 4 chunks per
+// partition also make 1024 workgroups = exactly two rounds of 2 per CU at 2^20 (2048 = four at 2^21)
+// where 12 K-entry chunks made 1280 (two and a half rounds).
 constexpr int SL_THREADS = 1024;
-#ifdef KGS_SL_FIXED16
-constexpr int SL_TILE = 4096;
-constexpr int SL_G = 16;
-constexpr uint32_t SL_CHUNK = 0;  // unused: always SL_G chunks
-#else
-constexpr int SL_TILE = 12288;
+constexpr int SL_TILE = 16384;
+constexpr int SL_TILE_BIG = SL_TILE / 2;  // tiles of the multi-tile (skewed) path: 8 entries per thread
 constexpr int SL_G = 64;
-constexpr uint32_t SL_CHUNK = 12288;
-#endif
+constexpr uint32_t SL_CHUNK = 16384;
+constexpr int LC_THREADS = 256;  // k_lo_count: one wave per sub-histogram
+constexpr int SL_HIST = LC_THREADS / 64;
 
 // chunks of a partition of `size` entries
 __device__ __forceinline__ uint32_t chunk_count(uint32_t size) {
-  if (SL_CHUNK == 0) return SL_G;
   const uint32_t g = (size + SL_CHUNK - 1) / SL_CHUNK;
   return g < 1 ? 1u : g > (uint32_t)SL_G ? (uint32_t)SL_G : g;
 }
@@ -311,17 +307,28 @@ __device__ __forceinline__ uint32_t chunk_count(uint32_t size) {
 // The lo-pass kernels run one workgroup per (partition, chunk) on a 1-D grid: cpre[p] = chunks of
 // the partitions before p (k_sort_scan), block b belongs to the partition p with
 // cpre[p] <= b < cpre[p + 1]; blocks past cpre[NH] (the host sizes the grid by an upper bound) exit.
-__device__ __forceinline__ bool chunk_of_block(const uint32_t* cpre, int NH, uint32_t b, uint32_t& p, uint32_t& g,
-                                               uint32_t& G) {
-  if (b >= cpre[NH]) return false;
-  uint32_t lo = 0, hi = (uint32_t)NH;  // cpre[lo] <= b < cpre[hi]
+// (p, g, G) of block b with one global round trip: the block stages cpre and hi_off (NH + 1 words each) in LDS
+// and searches there (the 8 dependent L2 loads of a global binary search cost microseconds per block);
+// also returns the partition's range [s0, s1). Called by every thread of the block.
+__device__ __forceinline__ bool chunk_of_block_lds(const uint32_t* __restrict__ cpre, const uint32_t* __restrict__ hi_off,
+                                                   int NH, uint32_t b, uint32_t* scp, uint32_t* shi, uint32_t& p,
+                                                   uint32_t& g, uint32_t& G, uint32_t& s0, uint32_t& s1) {
+  for (uint32_t t = threadIdx.x; t <= (uint32_t)NH; t += blockDim.x) {
+    scp[t] = cpre[t];
+    shi[t] = hi_off[t];
+  }
+  __syncthreads();
+  if (b >= scp[NH]) return false;
+  uint32_t lo = 0, hi = (uint32_t)NH;
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (cpre[mid] <= b) lo = mid; else hi = mid;
+    if (scp[mid] <= b) lo = mid; else hi = mid;
   }
   p = lo;
-  g = b - cpre[lo];
-  G = cpre[lo + 1] - cpre[lo];
+  g = b - scp[lo];
+  G = scp[lo + 1] - scp[lo];
+  s0 = shi[lo];
+  s1 = shi[lo + 1];
   return true;
 }
 
@@ -333,114 +340,173 @@ __device__ __forceinline__ void chunk_range(uint32_t s0, uint32_t s1, uint32_t G
 }
 
 // one block per (partition, chunk): locnt[(p * nb + lo) * SL_G + g] = #entries of chunk g of
-// partition p with this lo
-__global__ void __launch_bounds__(SL_THREADS) k_lo_count(uint32_t* __restrict__ locnt, const uint8_t* __restrict__ tlo,
+// partition p with this lo. 16-byte loads of the lo bytes (four in flight per thread), one
+// sub-histogram per wave against LDS atomic contention.
+__global__ void __launch_bounds__(LC_THREADS) k_lo_count(uint32_t* __restrict__ locnt, const uint8_t* __restrict__ tlo,
                                                          const uint32_t* __restrict__ hi_off,
                                                          const uint32_t* __restrict__ cpre, int NH, int lob) {
   KGS_AUX_PRIO();
-  __shared__ uint32_t cnt[256];
-  uint32_t p, g, G;
-  if (!chunk_of_block(cpre, NH, blockIdx.x, p, g, G)) return;  // uniform per block
+  __shared__ uint32_t cnt[SL_HIST][256];
+  __shared__ uint32_t scp[257], shi[257];
+  uint32_t p, g, G, s0, s1;
+  if (!chunk_of_block_lds(cpre, hi_off, NH, blockIdx.x, scp, shi, p, g, G, s0, s1)) return;  // uniform per block
   const int nb = 1 << lob;
-  const uint32_t s0 = hi_off[p], s1 = hi_off[p + 1];
+  const uint32_t tid = threadIdx.x;
   uint32_t c0, c1;
   chunk_range(s0, s1, G, g, c0, c1);
-  if ((int)threadIdx.x < nb) cnt[threadIdx.x] = 0;
+  for (uint32_t i = tid; i < SL_HIST * 256; i += LC_THREADS) (&cnt[0][0])[i] = 0;
   __syncthreads();
-  for (uint32_t e = c0 + threadIdx.x; e < c1; e += SL_THREADS) atomicAdd(&cnt[tlo[e]], 1u);
-  __syncthreads();
-  if ((int)threadIdx.x < nb) locnt[((uint64_t)p * nb + threadIdx.x) * SL_G + g] = cnt[threadIdx.x];
-}
-
-// grid NH, 256 threads: bases (in place over locnt) and the bucket offsets of keys (p << lob) + lo + 1
-__global__ void __launch_bounds__(256) k_lo_scan(uint32_t* __restrict__ locnt, uint32_t* __restrict__ offsets,
-                                                 const uint32_t* __restrict__ hi_off,
-                                                 const uint32_t* __restrict__ cpre, int lob) {
-  KGS_AUX_PRIO();
-  __shared__ uint32_t tot[256], pre[256];
-  const int p = blockIdx.x;
-  const int nb = 1 << lob;
-  const uint32_t G = cpre[p + 1] - cpre[p];
-  const uint32_t lo = threadIdx.x;
-  uint32_t* row = locnt + ((uint64_t)p * nb + lo) * SL_G;
-  uint32_t run = 0;
-  if ((int)lo < nb)
-    for (uint32_t g = 0; g < G; g++) {
-      const uint32_t v = row[g];
-      row[g] = run;
-      run += v;
+  uint32_t* h = cnt[tid >> 6];
+  const uint32_t a0 = ((c0 + 15) & ~15u) < c1 ? (c0 + 15) & ~15u : c1;
+  const uint32_t a1 = (c1 & ~15u) > a0 ? c1 & ~15u : a0;
+  if (c0 + tid < a0) atomicAdd(&h[tlo[c0 + tid]], 1u);  // head: < 16 bytes
+  if (a1 + tid < c1) atomicAdd(&h[tlo[a1 + tid]], 1u);  // tail: < 16 bytes
+  const uint4* q4 = reinterpret_cast<const uint4*>(tlo);
+  uint32_t q = a0 / 16 + tid;
+  for (; q + 3 * LC_THREADS < a1 / 16; q += 4 * LC_THREADS) {  // four 16-byte loads in flight
+    uint4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) x[u] = q4[q + u * LC_THREADS];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t w[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+#pragma unroll
+      for (int k = 0; k < 16; k++) atomicAdd(&h[(w[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
     }
-  tot[lo] = (int)lo < nb ? run : 0;
+  }
+  for (; q < a1 / 16; q += LC_THREADS) {
+    const uint4 x = q4[q];
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int k = 0; k < 16; k++) atomicAdd(&h[(w[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
+  }
   __syncthreads();
-  if (threadIdx.x < 64) wave_excl_scan256(tot, pre, nb);
-  __syncthreads();
-  if ((int)lo < nb) {
-    const uint32_t base = hi_off[p] + pre[lo];
-    offsets[((uint32_t)p << lob) + lo + 1] = base;
-    for (uint32_t g = 0; g < G; g++) row[g] += base;
+  if ((int)tid < nb) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < SL_HIST; k++) v += cnt[k][tid];
+    locnt[((uint64_t)p * nb + tid) * SL_G + g] = v;
   }
 }
 
-// one block per (partition, chunk): chunk g of partition p, tiles of SL_TILE through LDS, run-wise stores
-__global__ void __launch_bounds__(SL_THREADS) k_lo_scatter(uint32_t* __restrict__ sorted,
+// write the runs of a sorted LDS tile: bucket b's run sv[src[b], + n[b]) -> sorted[dst[b], ...). A
+// run of up to SL_BIGRUN entries is stored by one wave with consecutive lanes (uniform scalars: ~60
+// entries per bucket per chunk); longer runs (skewed scalars: one bucket holds the whole chunk) by
+// the whole block, so no wave is left with the tile while the others idle.
+constexpr uint32_t SL_BIGRUN = 512;
+// big[0, *nbig): the long runs found by the waves; *nbig is 0 on entry and on return
+__device__ __forceinline__ void lo_write_runs(uint32_t* __restrict__ sorted, const uint32_t* sv, const uint32_t* n,
+                                              const uint32_t* src, const uint32_t* dst, int nb, uint32_t* big,
+                                              uint32_t* nbig) {
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  for (uint32_t b = wave; b < (uint32_t)nb; b += SL_THREADS / 64) {
+    const uint32_t cnt = n[b];
+    if (cnt > SL_BIGRUN) {
+      if (lane == 0) big[atomicAdd(nbig, 1u)] = b;
+      continue;
+    }
+    const uint32_t s0 = src[b], d0 = dst[b];
+    for (uint32_t i = lane; i < cnt; i += 64) sorted[d0 + i] = sv[s0 + i];
+  }
+  __syncthreads();
+  const uint32_t nbg = *nbig;
+  for (uint32_t k = 0; k < nbg; k++) {
+    const uint32_t b = big[k], cnt = n[b], s0 = src[b], d0 = dst[b];
+    for (uint32_t i = tid; i < cnt; i += SL_THREADS) sorted[d0 + i] = sv[s0 + i];
+  }
+  __syncthreads();
+  if (tid == 0) *nbig = 0;
+}
+
+// one block per (partition, chunk): bases from the partition's chunk histograms, then chunk g of
+// partition p through LDS in tiles of SL_TILE (one tile unless the partition is skewed past SL_G
+// chunks), each bucket's run stored with consecutive lanes (lo_write_runs)
+__global__ void __launch_bounds__(SL_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lo_scatter(uint32_t* __restrict__ sorted, uint32_t* __restrict__ offsets,
                                                            const uint32_t* __restrict__ locnt,
                                                            const uint32_t* __restrict__ tval,
                                                            const uint8_t* __restrict__ tlo,
                                                            const uint32_t* __restrict__ hi_off,
                                                            const uint32_t* __restrict__ cpre, int NH, int lob) {
   KGS_AUX_PRIO();
-  __shared__ uint32_t cur[256], tcnt[256], toff[256];
+  __shared__ uint32_t cur[256], tcnt[256], toff[256], big[256];
+  __shared__ uint32_t scp[257], shi[257];
   __shared__ uint32_t sv[SL_TILE];
-  __shared__ uint8_t sl[SL_TILE];
-  uint32_t p, g, G;
-  if (!chunk_of_block(cpre, NH, blockIdx.x, p, g, G)) return;  // uniform per block
+  __shared__ uint32_t nbig;
+  if (threadIdx.x == 0) nbig = 0;
+  uint32_t p, g, G, s0, s1;
+  if (!chunk_of_block_lds(cpre, hi_off, NH, blockIdx.x, scp, shi, p, g, G, s0, s1)) return;  // uniform per block
   const uint32_t tid = threadIdx.x;
   const int nb = 1 << lob;
-  const uint32_t s0 = hi_off[p], s1 = hi_off[p + 1];
+  // global base of each lo in this chunk: partition start + entries of smaller lo (all chunks) +
+  // entries of this lo in earlier chunks; the chunk-0 block publishes the bucket offsets. The chunk's
+  // own counts (k_lo_count) give its LDS tile offsets up front.
+  __shared__ uint32_t ccnt[256], coff[256];
+  uint32_t pref = 0;
+  if ((int)tid < nb) {
+    const uint32_t* row = locnt + ((uint64_t)p * nb + tid) * SL_G;
+    uint32_t tot = 0;
+    for (uint32_t q = 0; q < G; q++) {
+      const uint32_t v = row[q];
+      pref += q < g ? v : 0u;
+      ccnt[tid] = q == g ? v : ccnt[tid];
+      tot += v;
+    }
+    tcnt[tid] = tot;
+  }
+  __syncthreads();
+  if (tid < 64) wave_excl_scan256(tcnt, toff, nb);
+  else if (tid < 128) wave_excl_scan256(ccnt, coff, nb);
+  __syncthreads();
+  if ((int)tid < nb) {
+    const uint32_t base = s0 + toff[tid];
+    if (g == 0) offsets[((uint32_t)p << lob) + tid + 1] = base;
+    cur[tid] = base + pref;
+    toff[tid] = coff[tid];  // slot cursor of lo in the LDS tile
+  }
   uint32_t c0, c1;
   chunk_range(s0, s1, G, g, c0, c1);
-  if (c0 >= c1) return;  // uniform per block
-  if ((int)tid < nb) cur[tid] = locnt[((uint64_t)p * nb + tid) * SL_G + g];
-  __syncthreads();
-  for (uint32_t t0 = c0; t0 < c1; t0 += SL_TILE) {
-    const uint32_t tn = c1 - t0 < (uint32_t)SL_TILE ? c1 - t0 : (uint32_t)SL_TILE;
-    if ((int)tid < nb) tcnt[tid] = 0;
+  if (c1 - c0 <= (uint32_t)SL_TILE) {
+    // the chunk is one tile (every partition of a non-skewed MSM): each entry goes straight to its
+    // slot (slot cursor per lo), then each bucket's run leaves with consecutive lanes
     __syncthreads();
-    uint32_t v[SL_TILE / SL_THREADS], r[SL_TILE / SL_THREADS];
-    uint8_t l[SL_TILE / SL_THREADS];
 #pragma unroll
     for (int k = 0; k < SL_TILE / SL_THREADS; k++) {
+      const uint32_t e = c0 + tid + k * SL_THREADS;
+      if (e < c1) sv[atomicAdd(&toff[tlo[e]], 1u)] = tval[e];
+    }
+    __syncthreads();
+    lo_write_runs(sorted, sv, ccnt, coff, cur, nb, big, &nbig);
+    return;
+  }
+  for (uint32_t t0 = c0; t0 < c1; t0 += SL_TILE_BIG) {
+    const uint32_t tn = c1 - t0 < (uint32_t)SL_TILE_BIG ? c1 - t0 : (uint32_t)SL_TILE_BIG;
+    __syncthreads();
+    if ((int)tid < nb) tcnt[tid] = 0;
+    __syncthreads();
+    // per entry (rank within its bucket << 8) | lo in one register; the values are loaded after the
+    // scan straight into their LDS slots (this path: skewed partitions only; the kernel stays within
+    // 64 VGPRs, two 1024-thread blocks per CU, without scratch)
+    uint32_t rl[SL_TILE_BIG / SL_THREADS];
+#pragma unroll
+    for (int k = 0; k < SL_TILE_BIG / SL_THREADS; k++) {
       const uint32_t e = tid + k * SL_THREADS;
       if (e < tn) {
-        l[k] = tlo[t0 + e];
-        v[k] = tval[t0 + e];
-        r[k] = atomicAdd(&tcnt[l[k]], 1u);
+        const uint32_t l = tlo[t0 + e];
+        rl[k] = (atomicAdd(&tcnt[l], 1u) << 8) | l;
       }
     }
     __syncthreads();
     if (tid < 64) wave_excl_scan256(tcnt, toff, nb);
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < SL_TILE / SL_THREADS; k++) {
+    for (int k = 0; k < SL_TILE_BIG / SL_THREADS; k++) {
       const uint32_t e = tid + k * SL_THREADS;
-      if (e < tn) {
-        const uint32_t q = toff[l[k]] + r[k];
-        sv[q] = v[k];
-        sl[q] = l[k];
-      }
+      if (e < tn) sv[toff[rl[k] & 255u] + (rl[k] >> 8)] = tval[t0 + e];
     }
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < SL_TILE / SL_THREADS; k++) {
-      const uint32_t e = tid + k * SL_THREADS;
-      if (e < tn) {
-        const uint32_t b = sl[e];
-        sorted[cur[b] + (e - toff[b])] = sv[e];
-      }
-    }
+    lo_write_runs(sorted, sv, tcnt, toff, cur, nb, big, &nbig);
     __syncthreads();
     if ((int)tid < nb) cur[tid] += tcnt[tid];
-    __syncthreads();
   }
 }
 
@@ -753,12 +819,10 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
       return;  // choose_c keeps 7 <= c <= 17
   }
   // lo-pass grid: an upper bound of sum_p chunk_count(size_p) (blocks past cpre[NH] exit)
-  const uint64_t chunk_bound = SL_CHUNK ? std::min<uint64_t>((uint64_t)NH * SL_G, NH + N * (uint64_t)W / SL_CHUNK)
-                                        : (uint64_t)NH * SL_G;
-  hipLaunchKernelGGL(k_lo_count, dim3((unsigned)chunk_bound), dim3(SL_THREADS), 0, st, w.locnt, w.lo, hi_off, cpre, NH,
+  const uint64_t chunk_bound = std::min<uint64_t>((uint64_t)NH * SL_G, NH + N * (uint64_t)W / SL_CHUNK);
+  hipLaunchKernelGGL(k_lo_count, dim3((unsigned)chunk_bound), dim3(LC_THREADS), 0, st, w.locnt, w.lo, hi_off, cpre, NH,
                      lob);
-  hipLaunchKernelGGL(k_lo_scan, dim3(NH), dim3(256), 0, st, w.locnt, w.offsets, hi_off, cpre, lob);
-  hipLaunchKernelGGL(k_lo_scatter, dim3((unsigned)chunk_bound), dim3(SL_THREADS), 0, st, w.sorted, w.locnt,
+  hipLaunchKernelGGL(k_lo_scatter, dim3((unsigned)chunk_bound), dim3(SL_THREADS), 0, st, w.sorted, w.offsets, w.locnt,
                      (const uint32_t*)w.digit, w.lo, hi_off, cpre, NH, lob);
   if (ev) hipEventRecord(ev[1], st);
   const uint64_t E = N * (uint64_t)W;  // upper bound of nonzero entries

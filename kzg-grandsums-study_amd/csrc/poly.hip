@@ -250,21 +250,21 @@ __global__ void __launch_bounds__(256) k_builder_finish(uint32_t* __restrict__ o
   fr sex = threadIdx.x < 255 ? fr::load(lds + 8 * (threadIdx.x + 1)) : fr::one();
   __syncthreads();
   fr inv = fr::load(tinv + 8 * (uint64_t)blockIdx.x) * pex * sex;  // 1/p
-  // backward: inv = 1 / (prefix_r * den_r) before step r, so num_r / den_r = np[r] * inv
-  fr* s = np;  // s_r overwrites np[r]
+  // backward: inv = 1 / (prefix_r * den_r) before step r, so num_r / den_r = np[r] * inv; s_r
+  // overwrites np[r]
 #pragma unroll
   for (int r = BT_PER - 1; r >= 0; r--) {
     if (den[r].is_zero()) {
-      s[r] = fr::zero();  // batchInverse(0) = 0 -> term 0
+      np[r] = fr::zero();  // batchInverse(0) = 0 -> term 0
     } else {
-      s[r] = np[r] * inv;
+      np[r] = np[r] * inv;
       inv = inv * den[r];
     }
   }
   // local inclusive scan inside thread, then across the tile
-  fr loc = s[0];
+  fr loc = np[0];
 #pragma unroll
-  for (int r = 1; r < BT_PER; r++) loc = PROD ? loc * s[r] : loc + s[r];
+  for (int r = 1; r < BT_PER; r++) loc = PROD ? loc * np[r] : loc + np[r];
   fr excl;
   if (PROD) {
     fr inc = block_scan_incl(loc, lds, OpMul());
@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(256) k_builder_finish(uint32_t* __restrict__ o
 #pragma unroll
   for (int r = 0; r < BT_PER; r++) {
     uint64_t i = base + r;
-    acc = PROD ? acc * s[r] : acc + s[r];
+    acc = PROD ? acc * np[r] : acc + np[r];
     if (i < n) {
       uint64_t j = i + 1 == n ? 0 : i + 1;
       acc.store(out + 8 * j);

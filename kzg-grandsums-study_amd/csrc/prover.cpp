@@ -138,7 +138,9 @@ uint32_t* get_nxm1(kgs_ctx& c, int nbits, int lcs) {
   const uint64_t cs = 1ull << lcs;
   uint32_t* out = c.buf("nxm1_" + std::to_string(nbits) + "_" + std::to_string(lcs), 32 * cs);
   uint32_t* tmp = c.buf("nxm1_tmp", 32 * cs);
-  Fr consts[2] = {Fr::from_u64(5), Fr::from_u64(1ull << nbits)};
+  // 1/(n (x - 1)) / cs: the coset inverse NTT of the quotient (coset_inv) takes its 1/cs from here and
+  // from the Z_H scalars of round 3 instead of a product per element
+  Fr consts[2] = {Fr::from_u64(5), Fr::from_u64(1ull << nbits) * Fr::from_u64(cs)};
   uint32_t* d = c.scal(consts, 2);
   // w_M^j (j < M/2) is the last stage table, tw_fwd + 8 * (M/2)
   const uint64_t halfM = (1ull << c.logM) / 2;
@@ -155,12 +157,12 @@ void intt_nat(kgs_ctx& c, uint32_t* out, const uint32_t* in, int logm, hipStream
   ntt_dit(st ? st : c.st, out, in, 0, logm, c.tw_inv, c.logM, nullptr, c.invm + 8 * logm);
 }
 // coefficients (len <= 2^lcs, natural) -> coset evaluations p(g w^i), bit-reversed order
-void coset_fwd(kgs_ctx& c, uint32_t* out, const uint32_t* in, uint64_t len, int lcs) {
-  ntt_dif(c.st, out, in, len, lcs, c.coset_pow, c.tw_fwd, c.logM);
+void coset_fwd(kgs_ctx& c, uint32_t* out, const uint32_t* in, uint64_t len, int lcs, hipStream_t st = nullptr) {
+  ntt_dif(st ? st : c.st, out, in, len, lcs, c.coset_pow, c.tw_fwd, c.logM);
 }
-// bit-reversed coset evaluations -> natural coefficients (in place allowed)
-void coset_inv(kgs_ctx& c, uint32_t* out, const uint32_t* in, int lcs) {
-  ntt_dit(c.st, out, in, 1, lcs, c.tw_inv, c.logM, c.coset_ipow, c.invm + 8 * lcs);
+// bit-reversed coset evaluations, already scaled by 1/cs -> natural coefficients (in place allowed)
+void coset_inv_prescaled(kgs_ctx& c, uint32_t* out, const uint32_t* in, int lcs) {
+  ntt_dit(c.st, out, in, 1, lcs, c.tw_inv, c.logM, c.coset_ipow, nullptr);
 }
 
 // ------------------------------------------------------------------ SRS
@@ -303,6 +305,14 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
 void shard_range(uint64_t n, int rank, int world, uint64_t& lo, uint64_t& hi) {
   lo = (uint64_t)((unsigned __int128)n * (unsigned)rank / (unsigned)world);
   hi = (uint64_t)((unsigned __int128)n * (unsigned)(rank + 1) / (unsigned)world);
+}
+
+// `to` waits for everything issued so far on `from` (lane hand-over inside a round)
+void lane_join(kgs_ctx& c, hipStream_t from, hipStream_t to) {
+  if (from == to) return;
+  if (!c.ev_join) HC(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
+  HC(hipEventRecord(c.ev_join, from));
+  HC(hipStreamWaitEvent(to, c.ev_join, 0));
 }
 
 // the second MSM lane starts after everything issued so far on the main stream (the round's inputs)
@@ -745,6 +755,18 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   std::vector<Fr> bpow(k);
   bpow[0] = Fr::one();
   for (int i = 1; i < k; i++) bpow[i] = bpow[i - 1] * beta;
+  // Two lanes (latency mode): the challenge-independent coset evaluations of F, T (+ selectors) run on
+  // lane 1 from the start of the round, beside the builder's serial part (k_tile_inverse is one
+  // workgroup) and S's inverse NTT on lane 0; S's commitment follows on lane 0, S's coset evaluation
+  // on lane 1 once S exists. One lane: the same work in order on the main stream.
+  fork_lanes(c);
+  hipStream_t s2 = c.msm_lanes >= 2 && c.st2 ? c.st2 : c.st;
+  const int lcs = (!gs && !sel) ? nbits : nbits + 1;
+  const uint64_t cs = 1ull << lcs;
+  uint32_t* cosS = c.buf("cosS", 32 * cs);
+  uint32_t* cosF = c.buf("cosF", 32 * cs);
+  uint32_t* cosT = c.buf("cosT", 32 * cs);
+  uint32_t *cosSF = nullptr, *cosST = nullptr;
   const uint32_t *fcomb = fm[0], *tcomb = tm[0], *polF = Fc[0], *polT = Tc[0];
   if (vec) {
     uint32_t* b_fe = c.buf("fcomb", E);
@@ -760,12 +782,20 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     }
     run_lincomb(c.st, b_fe, n, l1);
     run_lincomb(c.st, b_te, n, l2);
-    run_lincomb(c.st, b_F, n, l3);
-    run_lincomb(c.st, b_T, n, l4);
+    run_lincomb(s2, b_F, n, l3);
+    run_lincomb(s2, b_T, n, l4);
     fcomb = b_fe;
     tcomb = b_te;
     polF = b_F;
     polT = b_T;
+  }
+  coset_fwd(c, cosF, polF, n, lcs, s2);
+  coset_fwd(c, cosT, polT, n, lcs, s2);
+  if (sel) {
+    cosSF = c.buf("cosSF", 32 * cs);
+    cosST = c.buf("cosST", 32 * cs);
+    coset_fwd(c, cosSF, sFc, n, lcs, s2);
+    coset_fwd(c, cosST, sTc, n, lcs, s2);
   }
   uint32_t* Sev = c.buf("Sev", E);
   uint32_t* Sc = c.buf("Sc", E);
@@ -775,25 +805,9 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
                  c.buf("bt_ti", 32 * (ntiles + 1)), flags);
   intt_nat(c, Sc, Sev, nbits);
   check_launch();
-  // the S commitment runs on the second MSM lane while the main stream already computes round 3's
-  // challenge-independent coset evaluations of S, F, T (+ selectors)
-  fork_lanes(c);
-  Commit cS = commit_launch(c, Sc, n, slot++, 1);
-  const int lcs = (!gs && !sel) ? nbits : nbits + 1;
-  const uint64_t cs = 1ull << lcs;
-  uint32_t* cosS = c.buf("cosS", 32 * cs);
-  uint32_t* cosF = c.buf("cosF", 32 * cs);
-  uint32_t* cosT = c.buf("cosT", 32 * cs);
-  uint32_t *cosSF = nullptr, *cosST = nullptr;
-  coset_fwd(c, cosS, Sc, n, lcs);
-  coset_fwd(c, cosF, polF, n, lcs);
-  coset_fwd(c, cosT, polT, n, lcs);
-  if (sel) {
-    cosSF = c.buf("cosSF", 32 * cs);
-    cosST = c.buf("cosST", 32 * cs);
-    coset_fwd(c, cosSF, sFc, n, lcs);
-    coset_fwd(c, cosST, sTc, n, lcs);
-  }
+  lane_join(c, c.st, s2);
+  coset_fwd(c, cosS, Sc, n, lcs, s2);
+  Commit cS = commit_launch(c, Sc, n, slot++, 0);
   uint32_t* nxm1 = get_nxm1(c, nbits, lcs);
   check_launch();
   uint32_t* h_flags = (uint32_t*)c.pin(64);
@@ -814,12 +828,15 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   const uint64_t qlen = (!gs && !sel) ? n - 1 : 2 * n - 2;  // deg Q + 1 bound
   Fr gn = Fr::from_u64(5).pow_u64(n);
   // alpha_t: weight of the selT-binary term (none for a lookup, whose selT holds multiplicities)
-  Fr qs[5] = {alpha, gamma, (gn - Fr::one()).inverse(), (gn.neg() - Fr::one()).inverse(), lk ? Fr::zero() : alpha};
+  // 1/Z_H on the two coset halves, times 1/cs (the scaling of the inverse transform below; nxm1 carries it too)
+  const Fr inv_cs = Fr::from_u64(cs).inverse();
+  Fr qs[5] = {alpha, gamma, (gn - Fr::one()).inverse() * inv_cs, (gn.neg() - Fr::one()).inverse() * inv_cs,
+              lk ? Fr::zero() : alpha};
   uint32_t* d_qs = c.scal(qs, 5);
   launch_divcheck(c.st, !gs, sel, flags + 1, Sev, fcomb, tcomb, in.sel_f, in.sel_t, d_qs, n);
   uint32_t* Qc = c.buf("Qc", 32 * cs);
   launch_quotient(c.st, !gs, sel, Qc, cosS, cosF, cosT, cosSF, cosST, nxm1, d_qs, lcs, rot);
-  coset_inv(c, Qc, Qc, lcs);
+  coset_inv_prescaled(c, Qc, Qc, lcs);
   check_launch();
   // latency mode: Q's 2n points over both MSM lanes (one lane's sort and tail overlap the other's
   // accumulation)
@@ -915,9 +932,15 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   L = qlen > n ? qlen : n;
   Pbuf = c.buf("Pw", 32 * L);
   uint32_t* Wx = c.buf("Wxi", 32 * L);
+  const uint32_t* xp1 = xpowers(c, xi);
+  const uint32_t* xp2 = xpowers(c, xiw);
+  // two lanes: W_x's linear combination and division on lane 0 while W_xw's run on lane 1 (and its
+  // commitment starts there right after); the commitments balance as W_x[0, h) on lane 0 and W_xw +
+  // W_x[h, L - 1) on lane 1, h = half of all their points
+  fork_lanes(c);
   run_lincomb(c.st, Pbuf, L, lw);
   const uint32_t dtiles = (uint32_t)((L + EVAL_TILE - 1) / EVAL_TILE);
-  launch_divide(c.st, Wx, flags + 2, Pbuf, L, xpowers(c, xi), c.buf("div_part", 32 * (dtiles + 1)),
+  launch_divide(c.st, Wx, flags + 2, Pbuf, L, xp1, c.buf("div_part", 32 * (dtiles + 1)),
                 c.buf("div_carry", 32 * (dtiles + 1)));
   // W_{xi w} = (S - S(xi w)) / (X - xi w)
   LcTerms l2;
@@ -925,14 +948,12 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   l2.c0 = sxiw.neg();
   uint32_t* P2 = c.buf("Pw2", E);
   uint32_t* Wxw = c.buf("Wxiw", E);
-  run_lincomb(c.st, P2, n, l2);
-  launch_divide(c.st, Wxw, flags + 3, P2, n, xpowers(c, xiw), c.buf("div_part2", 32 * (ntiles + 1)),
+  run_lincomb(s2, P2, n, l2);
+  launch_divide(s2, Wxw, flags + 3, P2, n, xp2, c.buf("div_part2", 32 * (ntiles + 1)),
                 c.buf("div_carry2", 32 * (ntiles + 1)));
   check_launch();
-  fork_lanes(c);
-  // two lanes: W_xw (n - 1 points) and W_x (L - 1) balanced as W_x[0, h) on lane 0 and W_xw +
-  // W_x[h, L - 1) on lane 1, h = half of all their points
   Commit cW2 = commit_launch(c, Wxw, n - 1, slot++, 1);
+  lane_join(c, c.st, s2);  // W_x[h, L - 1) on lane 1 needs W_x
   Commit cW1 = commit_launch_split(c, Wx, L - 1, (L - 1 + n - 1) / 2, slot);
   slot += 2;
   HC(hipMemcpyAsync(h_flags, flags, 64, hipMemcpyDeviceToHost, c.st));

@@ -136,6 +136,30 @@ def test_msm_skewed_buckets(K):
     ctx.close()
 
 
+def test_msm_skewed_multitile_linearity(K):
+    """2^21 equal scalars: each window's 2^21 entries land in ONE bucket, so each partition is cut into
+    SL_G chunks of 32 K entries, more than one LDS tile (k_lo_scatter's multi-tile path). Checked by
+    linearity against two MSMs of random (non-skewed, single-tile) scalars: msm(a) = msm(r) + msm(a - r)."""
+    nbits = 21
+    n = 1 << nbits
+    path = f"/tmp/kgs_test_gpu_p{nbits}.ptau"
+    ctx = K.Context(0)
+    if not os.path.exists(path):
+        ctx.write_synthetic_ptau(path, nbits, common.tau())
+    ctx.load_ptau(path, nbits)
+    rnd = random.Random(2121)
+    a = rnd.randrange(R)
+    rs = [rnd.randrange(R) for _ in range(n)]
+    # Montgomery forms are linear: (a - r) of the byte values is the Montgomery form of the difference
+    eq = a.to_bytes(32, "little") * n
+    rb = b"".join(x.to_bytes(32, "little") for x in rs)
+    db = b"".join(((a - x) % R).to_bytes(32, "little") for x in rs)
+    p_eq = bn.g1_from_lem(ctx.msm(eq))
+    p_sum = bn.g1_add(bn.g1_from_lem(ctx.msm(rb)), bn.g1_from_lem(ctx.msm(db)))
+    assert p_eq == p_sum
+    ctx.close()
+
+
 @pytest.mark.parametrize("kind", [0, 1])
 @pytest.mark.parametrize("sel", [False, True])
 @pytest.mark.parametrize("nbits", [1, 4, 11, 13])
