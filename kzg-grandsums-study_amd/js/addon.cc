@@ -125,10 +125,11 @@ uint8_t* out_alloc(size_t len) {
   const uintptr_t end = (uintptr_t)raw + sz + HUGE;
   if (end > a + sz) munmap((void*)(a + sz), end - (a + sz));
   madvise((void*)a, sz, MADV_HUGEPAGE);
-  // pinned for the whole life of the buffer: kgs_prove then DMAs the Montgomery write-back straight
-  // into it (no per-call registration, no staging copy); unpinned before it is unmapped
-  static const bool no_reg = getenv("KGS_JS_NO_OUT_REGISTER") != nullptr;  // A/B switch
-  if (!no_reg) kgs_host_register((void*)a, sz);
+  // KGS_JS_OUT_REGISTER=1: pin the buffer for its life (kgs_host_register) so the Montgomery
+  // write-back is DMA'd in place. Off by default: registering a fresh 32 MiB buffer costs more than
+  // the staging copy it saves whenever the caller keeps its outputs (profiles/r03/boundary_ab.txt)
+  static const bool reg = getenv("KGS_JS_OUT_REGISTER") != nullptr;
+  if (reg) kgs_host_register((void*)a, sz);
   return (uint8_t*)a;
 }
 
@@ -142,8 +143,8 @@ void out_release(uint8_t* p, size_t len) {
       return;
     }
   }
-  static const bool no_reg = getenv("KGS_JS_NO_OUT_REGISTER") != nullptr;
-  if (!no_reg) kgs_host_unregister(p);
+  static const bool reg = getenv("KGS_JS_OUT_REGISTER") != nullptr;
+  if (reg) kgs_host_unregister(p);
   munmap(p, sz);
 }
 }  // namespace

@@ -3,7 +3,7 @@
 // Inputs are random standard-form field elements (< 2^253 < r) in Uint8Arrays, T = F rotated by one
 // element, prepared before the timed regions (the prover overwrites them with Montgomery form, so
 // every proof gets its own copy).
-//  * latency: one proof at a time, best of PROOFS;
+//  * latency: one proof at a time, back to back (inputs prepared beforehand), best of PROOFS;
 //  * concurrent throughput: PROOFS * CONCURRENCY proofs issued as CONCURRENCY independent chains of
 //    awaited prover() calls (the reference API is async; independent calls run on the backend's
 //    context pool), wall clock of the whole batch.
@@ -27,8 +27,11 @@ const { poolInfo, diag } = require("../src/backend");
     let [F, T] = mk();
     let proof = await mset_eq_kzg_grandsum_prover(ptau, F, T);  // warm: context, SRS, buffers
     let best = Infinity, bestDiag = null;
+    // fresh standard-form inputs per proof (the prover overwrites them with Montgomery form), all made
+    // before the timed loop so the proofs run back to back, as the Python latency probe's do
+    const lat = Array.from({ length: proofs }, mk);
     for (let i = 0; i < proofs; i++) {
-        [F, T] = mk();  // fresh standard-form inputs (the prover overwrites them with Montgomery form)
+        [F, T] = lat[i];
         const t0 = process.hrtime.bigint();
         proof = await mset_eq_kzg_grandsum_prover(ptau, F, T);
         const ms = Number(process.hrtime.bigint() - t0) / 1e6;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Host-buffer boundary A/B: per-call registration of caller buffers (KGS_HOST_REGISTER=1) vs pinned
 # staging (default) vs caller-pinned inputs (probe line host_prereg); JS output buffers registered
-# for their life (default) vs not (KGS_JS_NO_OUT_REGISTER=1).
+# for their life (KGS_JS_OUT_REGISTER=1; the default when this ran, opt-in since) vs not.
 set -e
 cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03e
@@ -14,7 +14,7 @@ KGS_HOST_REGISTER=1 timeout -k 10 200 python3 profiles/boundary_probe.py 20 5 > 
 cat $OUT/boundary_percall.txt
 P=/tmp/kgs_bench_p20.ptau
 for v in outreg outnoreg outreg2 outnoreg2; do
-  E=""; case $v in outnoreg*) E="KGS_JS_NO_OUT_REGISTER=1";; esac
+  E="KGS_JS_NO_REG=0"; case $v in outreg*) E="KGS_JS_OUT_REGISTER=1";; esac
   env $E KGS_JS_CONTEXTS=8 KGS_DEVICES=0 timeout -k 10 300 node kzg-grandsums-study_amd/js/test/time_prove.js $P 20 5 16 > $OUT/js_$v.json
   echo "$v $(cat $OUT/js_$v.json)"
 done
