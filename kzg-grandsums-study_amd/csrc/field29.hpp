@@ -20,11 +20,22 @@
 #pragma once
 #include "field.hpp"
 
+// CIOS rows that take the 32-bit m of fq29::reduce_row32 (at most 8: row 8 keeps the 29-bit m; the
+// column bounds are re-derived by tests/test_field29.py); 0 builds the all-29-bit-m products for A/B
+#ifndef KGS_M32_ROWS
+#define KGS_M32_ROWS 8
+#endif
+#ifndef KGS_M32_ROWS_MUL2
+#define KGS_M32_ROWS_MUL2 8
+#endif
+static_assert(KGS_M32_ROWS <= 8 && KGS_M32_ROWS_MUL2 <= 8, "column bounds of fq29::reduce_row32");
+
 namespace kgs {
 namespace f29 {
 
 constexpr uint32_t MASK = 0x1fffffffu;
-constexpr uint32_t INV = 0x04866389u;  // -q^-1 mod 2^29
+constexpr uint32_t INV = 0x04866389u;    // -q^-1 mod 2^29
+constexpr uint32_t INV32 = 0x24866389u;  // -q0^-1 mod 2^32 (q0 = Q.v[0]; = INV mod 2^29)
 struct L9 {
   uint32_t v[9];
 };
@@ -144,11 +155,41 @@ struct fq29 {
     t[0] += c;
     t[8] = 0;
   }
+  // The same step with a 32-bit m = -t0/q0 mod 2^32 (no mask): t0 + m*q0 then has 32 zero low bits,
+  // so its carry into the next column, (t0 + m*q0) >> 29, is 8 x its high word — one v_mad_u64_u32
+  // (8 comes in an SGPR the compiler cannot fold into a shift) instead of a 64-bit shift, a 64-bit add
+  // and the mask: 3 instead of 5 VALU per row. m < 2^32 adds < 2^(29 i + 32) q to the reduced value in
+  // row i, so rows 0..7 take it (together < 2^-25 q over the 2^261 of the division) and row 8 keeps
+  // the 29-bit m (the result stays < a*b/2^261 + q(1 + 2^-25)). Columns: mul/sqr of normalised
+  // operands < 2^63.0 (outputs < 2^62.6, read as int64 by carry_sub); mul2 with add_aff's / add's
+  // operand limb bounds < 2^64 — tests/test_field29.py re-derives every column bound row by row and
+  // runs the exact row schedule on Python integers.
+  __device__ __forceinline__ static void reduce_row32(uint64_t (&t)[9], uint32_t eight) {
+    const uint32_t m = (uint32_t)t[0] * f29::INV32;
+    const uint64_t u = (uint64_t)m * f29::Q.v[0] + t[0];
+#pragma unroll
+    for (int j = 1; j < 9; j++) t[j] = (uint64_t)m * f29::Q.v[j] + t[j];
+#pragma unroll
+    for (int j = 0; j < 8; j++) t[j] = t[j + 1];
+    t[0] = (uint64_t)(uint32_t)(u >> 32) * eight + t[0];
+    t[8] = 0;
+  }
+  // 8 as an opaque SGPR value (keeps reduce_row32's carry a v_mad_u64_u32)
+  __device__ __forceinline__ static uint32_t opaque8() {
+    uint32_t e = 8;
+    asm volatile("" : "+s"(e));
+    return e;
+  }
+  template <int M32_ROWS>
+  __device__ __forceinline__ static void reduce_row_at(uint64_t (&t)[9], int i, uint32_t eight) {
+    if (i < M32_ROWS) reduce_row32(t, eight); else reduce_row(t);
+  }
 
   // Montgomery product a*b*2^-261 (CIOS, 64-bit column accumulators, no carry words).
-  // Needs 9*max(a_j)*max(b_j) + 9*(2^29)^2 + 2^36 < 2^64 (e.g. a_j < 2^29, b_j < 2^30.6) and
-  // a*b < 2^261 * (2^261 - q); the result is < a*b/2^261 + q.
+  // Needs 9*max(a_j)*max(b_j) + 2^32 * sum(q_j) + 2^36 < 2^64 (a_j, b_j < 2^29; reduce_row32 in
+  // rows 0..7) and a*b < 2^261 * (2^261 - q); the result is < a*b/2^261 + q(1 + 2^-25).
   __device__ __forceinline__ static cols mul_cols(const fq29& a, const fq29& b) {
+    const uint32_t eight = opaque8();
     cols r;
 #pragma unroll
     for (int j = 0; j < 9; j++) r.t[j] = 0;
@@ -156,7 +197,7 @@ struct fq29 {
     for (int i = 0; i < 9; i++) {
 #pragma unroll
       for (int j = 0; j < 9; j++) r.t[j] = (uint64_t)a.l[i] * b.l[j] + r.t[j];
-      reduce_row(r.t);
+      reduce_row_at<KGS_M32_ROWS>(r.t, i, eight);
     }
     return r;
   }
@@ -166,6 +207,7 @@ struct fq29 {
   // absolute columns 2i..i+8, which sit at t[i..8] after i shifts. A column receives at most 5
   // products (<= 2 * max(a_j)^2 each), so it stays below mul's bound for a normalised a.
   __device__ __forceinline__ static cols sqr_cols(const fq29& a) {
+    const uint32_t eight = opaque8();
     uint32_t d[9];
 #pragma unroll
     for (int j = 0; j < 9; j++) d[j] = a.l[j] << 1;
@@ -177,7 +219,7 @@ struct fq29 {
       r.t[i] = (uint64_t)a.l[i] * a.l[i] + r.t[i];
 #pragma unroll
       for (int j = i + 1; j < 9; j++) r.t[j] = (uint64_t)d[i] * a.l[j] + r.t[j];
-      reduce_row(r.t);
+      reduce_row_at<KGS_M32_ROWS>(r.t, i, eight);
     }
     return r;
   }
@@ -187,6 +229,7 @@ struct fq29 {
   // Needs 9*(max a_j * max b_j + max c_j * max d_j) + 9*(2^29)^2 + 2^36 < 2^64 (a and c normalised)
   // and a*b + c*d < 2^261 * (2^261 - q); the result is < (a*b + c*d)/2^261 + q.
   __device__ __forceinline__ static cols mul2_cols(const fq29& a, const fq29& b, const fq29& c2, const fq29& d2) {
+    const uint32_t eight = opaque8();
     cols r;
 #pragma unroll
     for (int j = 0; j < 9; j++) r.t[j] = 0;
@@ -196,7 +239,7 @@ struct fq29 {
       for (int j = 0; j < 9; j++) r.t[j] = (uint64_t)a.l[i] * b.l[j] + r.t[j];
 #pragma unroll
       for (int j = 0; j < 9; j++) r.t[j] = (uint64_t)c2.l[i] * d2.l[j] + r.t[j];
-      reduce_row(r.t);
+      reduce_row_at<KGS_M32_ROWS_MUL2>(r.t, i, eight);
     }
     return r;
   }

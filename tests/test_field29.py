@@ -46,6 +46,10 @@ def test_constants():
     assert _d32(_words("C261W[8]", t)) == pow(2, 261, Q)
     inv = int(re.search(r"INV = (0x[0-9a-f]+)u", t).group(1), 16)
     assert (Q * inv) % (1 << 29) == (1 << 29) - 1  # -q^-1 mod 2^29
+    inv32 = int(re.search(r"INV32 = (0x[0-9a-f]+)u", t).group(1), 16)
+    q0 = _words("L9 Q", t)[0]
+    assert (q0 * inv32) % (1 << 32) == (1 << 32) - 1  # -q0^-1 mod 2^32 (reduce_row32)
+    assert inv32 % (1 << 29) == inv
 
 
 def _spread(k, s):
@@ -67,30 +71,72 @@ class V:
         return min(self.limb, (self.val - 1) >> (29 * j)) if j == 8 else self.limb
 
 
-def _mul(a, b):
-    col = 9 * a.limb * b.limb + 9 * MASK * MASK + (1 << 36)
-    assert col < (1 << 64), "column overflow %.3f" % math.log2(col)
-    out = (a.val * b.val >> RBITS) + Q + 1
+QL = [(Q >> (29 * j)) & MASK for j in range(8)] + [Q >> 232]
+
+
+def _m32_rows():
+    """KGS_M32_ROWS / KGS_M32_ROWS_MUL2 of the header: CIOS rows that take reduce_row32's 32-bit m"""
+    t = _hdr()
+    return (int(re.search(r"#define KGS_M32_ROWS (\d+)", t).group(1)),
+            int(re.search(r"#define KGS_M32_ROWS_MUL2 (\d+)", t).group(1)))
+
+
+def _col_bounds(rows, m32):
+    """upper bounds of the CIOS column accumulators: rows(i) -> [(column, max product)] added in row
+    i; rows < m32 reduce with m < 2^32 (reduce_row32), the others with m < 2^29. Returns (largest
+    accumulator value at any point, largest output column)."""
+    t, worst = [0] * 9, 0
+    for i in range(9):
+        for j, p in rows(i):
+            t[j] += p
+        m = (1 << (32 if i < m32 else 29)) - 1
+        u = m * QL[0] + t[0]
+        worst = max(worst, u, max(t))
+        for j in range(1, 9):
+            t[j] += m * QL[j]
+        worst = max(worst, max(t))
+        t = t[1:] + [0]
+        t[0] += u >> 29
+    return worst, max(t)
+
+
+def _limbs_max(a):
+    return [a.limb_max(j) for j in range(9)]
+
+
+def _out(s):
+    # (s + M q) / 2^261 with M = sum m_i 2^(29 i): m_i < 2^32 in rows 0..7 add < 2^-25 q
+    out = (s >> RBITS) + Q + (Q >> 25) + 1
     assert out <= (1 << RBITS)
     return V(out, MASK)
 
 
-def _sqr(a):  # fq29::sqr: <= 5 products per column, each <= 2 * limb^2
-    col = 10 * a.limb * a.limb + 9 * MASK * MASK + (1 << 36)
-    assert col < (1 << 64), "column overflow %.3f" % math.log2(col)
-    out = (a.val * a.val >> RBITS) + Q + 1
-    assert out <= (1 << RBITS)
-    return V(out, MASK)
+def _mul(a, b, fused=False):
+    al, bl = _limbs_max(a), _limbs_max(b)
+    worst, outc = _col_bounds(lambda i: [(j, al[i] * bl[j]) for j in range(9)], _m32_rows()[0])
+    assert worst < (1 << 64), "column overflow %.3f" % math.log2(worst)
+    if fused:
+        _fused(outc)
+    return _out(a.val * b.val)
+
+
+def _sqr(a, fused=False):  # fq29::sqr: row i adds a_i^2 at column 2i and 2 a_i a_j at i + j
+    al = _limbs_max(a)
+    worst, outc = _col_bounds(lambda i: [(i, al[i] * al[i])] + [(j, 2 * al[i] * al[j]) for j in range(i + 1, 9)],
+                              _m32_rows()[0])
+    assert worst < (1 << 64), "column overflow %.3f" % math.log2(worst)
+    if fused:
+        _fused(outc)
+    return _out(a.val * a.val)
 
 
 def _mul2(a, b, c, d):  # fq29::mul2: (a*b + c*d) / 2^261, one reduction
-    col = 9 * (a.limb * b.limb + c.limb * d.limb) + 9 * MASK * MASK + (1 << 36)
-    assert col < (1 << 64), "column overflow %.3f" % math.log2(col)
+    al, bl, cl, dl = _limbs_max(a), _limbs_max(b), _limbs_max(c), _limbs_max(d)
+    worst, _ = _col_bounds(lambda i: [(j, al[i] * bl[j] + cl[i] * dl[j]) for j in range(9)], _m32_rows()[1])
+    assert worst < (1 << 64), "column overflow %.3f" % math.log2(worst)
     s = a.val * b.val + c.val * d.val
     assert s < (1 << RBITS) * ((1 << RBITS) - Q)
-    out = (s >> RBITS) + Q + 1
-    assert out <= (1 << RBITS)
-    return V(out, MASK)
+    return _out(s)
 
 
 def _fused(cols_bound):
@@ -99,13 +145,11 @@ def _fused(cols_bound):
 
 
 def _mul_cols(a, b):
-    _fused(9 * a.limb * b.limb + 9 * MASK * MASK + (1 << 36))
-    return _mul(a, b)
+    return _mul(a, b, fused=True)
 
 
 def _sqr_cols(a):
-    _fused(10 * a.limb * a.limb + 9 * MASK * MASK + (1 << 36))
-    return _sqr(a)
+    return _sqr(a, fused=True)
 
 
 def _add(a, b):
@@ -237,18 +281,27 @@ def test_pack_unpack_roundtrip_model():
         assert out == w
 
 
-def _cios(rows):
+def _cios(rows, m32):
     """fq29 CIOS loop of mul/sqr/mul2 on Python ints: rows(i) -> list of (absolute column offset j,
-    product) pairs added in row i; every 64-bit column accumulator is checked for overflow."""
+    product) pairs added in row i; rows < m32 run reduce_row32 (m = -t0/q0 mod 2^32 from the low
+    word, carry = 8 x the high word of t0 + m q0), the others reduce_row; every 64-bit column
+    accumulator is checked for overflow."""
     qv = [(Q >> (29 * j)) & MASK for j in range(8)] + [Q >> 232]
     inv = (-pow(Q, -1, 1 << 29)) % (1 << 29)
+    inv32 = (-pow(qv[0], -1, 1 << 32)) % (1 << 32)
     t = [0] * 9
     for i in range(9):
         for j, p in rows(i):
             t[j] += p
             assert t[j] < (1 << 64)
-        m = (t[0] * inv) & MASK
-        c = (m * qv[0] + t[0]) >> 29
+        if i < m32:
+            m = ((t[0] & 0xffffffff) * inv32) & 0xffffffff
+            u = m * qv[0] + t[0]
+            assert u < (1 << 64) and u % (1 << 32) == 0
+            c = 8 * (u >> 32)
+        else:
+            m = (t[0] * inv) & MASK
+            c = (m * qv[0] + t[0]) >> 29
         for j in range(1, 9):
             t[j] += m * qv[j]
             assert t[j] < (1 << 64)
@@ -268,21 +321,28 @@ def _limbs(x):
 
 
 def test_sqr_mul2_model():
-    # the exact row schedules of fq29::sqr and fq29::mul2 on random inputs at their bound limits
+    # the exact row schedules of fq29::mul, fq29::sqr and fq29::mul2 (with the header's 32-bit-m rows)
+    # on random inputs at their bound limits, and the all-limbs-maximal worst case
     import random
     rnd = random.Random(11)
     rinv = pow(2, -261, Q)
-    for _ in range(300):
-        a = rnd.randrange(1 << 258)
-        al = _limbs(a)
+    m32, m32_mul2 = _m32_rows()
+    big = (1 << 258) - 1
+    for it in range(300):
+        a = big if it == 0 else rnd.randrange(1 << 258)
+        b0 = big if it == 0 else rnd.randrange(1 << 258)
+        al, b0l = _limbs(a), _limbs(b0)
         d = [2 * x for x in al]
-        sq = _cios(lambda i: [(i, al[i] * al[i])] + [(j, d[i] * al[j]) for j in range(i + 1, 9)])
-        assert sq % Q == a * a * rinv % Q and sq < (a * a >> 261) + Q + 1
+        sq = _cios(lambda i: [(i, al[i] * al[i])] + [(j, d[i] * al[j]) for j in range(i + 1, 9)], m32)
+        assert sq % Q == a * a * rinv % Q and sq < (a * a >> 261) + Q + (Q >> 25) + 1
+        mu = _cios(lambda i: [(j, al[i] * b0l[j]) for j in range(9)], m32)
+        assert mu % Q == a * b0 * rinv % Q and mu < (a * b0 >> 261) + Q + (Q >> 25) + 1
         # mul2 with unnormalised second factors (limbs up to 2^30.6 / 2^29.8 as in add_aff)
         b, c, e = rnd.randrange(1 << 258), rnd.randrange(1 << 258), rnd.randrange(1 << 255)
         bl, cl, el = _limbs(b), _limbs(c), _limbs(e)
         bl = [x + (1 << 30) if j < 8 else x for j, x in enumerate(bl)]  # same value + spread carries
         bl = [bl[0]] + [bl[j] - 2 if j < 8 else bl[j] - 2 for j in range(1, 9)]
         bval = _d29(bl)
-        m2 = _cios(lambda i: [(j, al[i] * bl[j]) for j in range(9)] + [(j, cl[i] * el[j]) for j in range(9)])
+        m2 = _cios(lambda i: [(j, al[i] * bl[j]) for j in range(9)] + [(j, cl[i] * el[j]) for j in range(9)],
+                   m32_mul2)
         assert m2 % Q == (a * bval + c * e) * rinv % Q
