@@ -78,12 +78,15 @@ def log(msg):
     """progress on stderr (stdout carries only the JSON line)"""
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
-# v_mad_u64_u32 issue rate of the whole chip: 256 CUs x 4 SIMDs x 64 lanes / MAD_CYCLES x 2.4 GHz
-# (measured: profiles/ubench/issue_rates.hip; the fastest of the boxes measured). One bucket add
-# (madd-2008-s in 9 x 29-bit limbs, field29.hpp) issues 1,467 of them: 6 products x 162, 2 squares x
-# 126 (45 symmetric partial products + 81 for the reduction), and Y3 = R*T - Y1*PPP as one lazily
-# reduced double product (243)
-MAD_CYCLES = 4.93  # ubench_r02.txt issue_rates (5.25 on the round-1 box: ubench_r01.txt)
+# v_mad_u64_u32 issue rate of the whole chip: 256 CUs x 4 SIMDs x 64 lanes / MAD_CYCLES x 2.4 GHz.
+# MAD_CYCLES = 4: the architectural full rate of a wave64 VALU instruction on a 16-lane SIMD, which
+# v_mad_u64_u32 reaches when its carry-out goes to an ordinary SGPR pair, as the compiler emits it
+# (profiles/ubench/issue_rates2_r03.txt: 4.16 SIMD cycles including loop overhead, the same as every
+# other full-rate VOP3 op; the 4.93 of ubench_r02.txt wrote VCC). One bucket add (madd-2008-s in
+# 9 x 29-bit limbs, field29.hpp) issues 1,467 partial-product mads: 6 products x 162, 2 squares x 126
+# (45 symmetric partial products + 81 for the reduction), and Y3 = R*T - Y1*PPP as one lazily reduced
+# double product (243); the 8 carry mads per product of fq29::reduce_row32 are reduction overhead
+MAD_CYCLES = 4.0
 MAD_PEAK = 256 * 4 * 64 / MAD_CYCLES * 2.4e9
 MADS_PER_ADD = 6 * 162 + 2 * 126 + 243
 # mads per 254-bit Montgomery product: 9 x 29-bit CIOS (81 a*b + 81 m*q, the kernel's form) and the
@@ -522,11 +525,12 @@ def main():
                 "frac_at_held_clock": round(achieved / (peak * ghz / 2.4), 4),
                 "simd_cycles_per_valu_instruction": clock.get("simd_cycles_per_valu_instruction"),
                 "issue_frac_vs_register_resident_add": clock.get("issue_frac_vs_register_resident_add"),
-                "note": "counter passes (profiles/clock_accumulate.json, real cycles = GRBM_GUI_ACTIVE/8): the chip holds "
-                        "~2.07 GHz under this kernel, not 2.4; it issues one VALU instruction per ~4.73 SIMD cycles, "
-                        "against 4.17 for the same add arithmetic register-resident (madd29 ubench): 88 % of its "
-                        "arithmetic's issue rate; the rest of `peak` is the carries and reductions around the mads "
-                        "(DESIGN.md §3)"}
+                "note": (f"counter passes (profiles/clock_accumulate.json, real cycles = GRBM_GUI_ACTIVE/8): the chip "
+                         f"holds ~{ghz:.2f} GHz under this kernel, not 2.4; it issues one VALU instruction per "
+                         f"~{clock.get('simd_cycles_per_valu_instruction')} SIMD cycles, against "
+                         f"{clock.get('register_resident_add_cpi')} for the same add arithmetic register-resident "
+                         f"(madd29 ubench); the rest of `peak` is the carries and reductions around the mads "
+                         f"(DESIGN.md §3)")}
 
         # ---------------- proof-level HBM view (north star: achieved HBM-bandwidth fraction). Bytes per
         # proof = SURVEY.md §8d's count over the REFERENCE op list, B_gs(n) = 131 E = 4192 n (grand-sum,

@@ -588,38 +588,54 @@ __global__ void __launch_bounds__(256, VW) k_accumulate(uint32_t* __restrict__ s
     if (offsets[mid] <= start) lo = mid; else hi = mid;
   }
   uint32_t b = lo;
+  const uint32_t o0 = offsets[b], o1 = offsets[b + 1];
   segowner[s] = b;  // bucket of the segment's first run (read by the combine levels)
-  combine_enqueue(chunklist, chunkcnt, s, offsets[b], offsets[b + 1], L, 1);
+  combine_enqueue(chunklist, chunkcnt, s, o0, o1, L, 1);
   g1_acc29 acc;
   acc.set_inf();
   // entry indices fit 32 bits (offsets[] is uint32): fewer live VGPRs in the add loop
-  const uint32_t end32 = (uint32_t)end;
-  uint32_t rs32 = (uint32_t)start, bend32 = offsets[b + 1];
-  // software pipeline: the point of entry e+1 and the index of entry e+2 are in flight while
-  // entry e is added (the gathers' latency hides behind ~11 K cycles of VALU work)
+  const uint32_t end32 = (uint32_t)end, last = end32 - 1;
+  // record of the current run: b if it starts its bucket, nbins + s for the segment's first run when
+  // the segment starts inside the bucket (every later run starts at a bucket boundary)
+  uint32_t rec = (uint32_t)start == o0 ? b : nbins + (uint32_t)s;
+  // bucket ends: bend32 of bucket b and bnext of bucket b + 1, re-read after every entry (a 4-byte
+  // cache hit, first needed at the next crossing), so a crossing (some lane of the wave makes one in
+  // about half of the iterations at 2^20 points) waits on no load; only empty buckets read offsets[]
+  // on the spot
+  uint32_t bend32 = o1, bnext = offsets[b + 2 <= nbins ? b + 2 : nbins];
+  // software pipeline: the point of entry e+1 and the index of entry e+2 are loaded while entry e is
+  // added, UNCONDITIONALLY (indices clamped to the segment's last entry): a conditional prefetch is
+  // merged into the loop-carried registers by copies placed right after the loads, and the copies made
+  // the wave wait for the gathers it had just issued; here the copies sit at the loop latch, after
+  // the add
   uint32_t v = sorted[start];
-  uint32_t vn = start + 1 < end ? sorted[start + 1] : 0u;
+  uint32_t vn = sorted[start + 1 <= last ? start + 1 : last];
   const uint4* pt = reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(v & KGS_DIAG_GATHER_MASK));
   uint4 a0 = pt[0], a1 = pt[1], a2 = pt[2], a3 = pt[3];
-  for (uint32_t e = (uint32_t)start; e < end32; e++) {
+  for (uint32_t e = (uint32_t)start; e <= last; e++) {
+    const uint4* pn = reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(vn & KGS_DIAG_GATHER_MASK));
+    const uint4 n0 = pn[0], n1 = pn[1], n2 = pn[2], n3 = pn[3];
+    const uint32_t vnn = sorted[e + 2 <= last ? e + 2 : last];
     if (e >= bend32) {
-      acc.store_raw(run_rec(raw, rs32 == offsets[b] ? (uint64_t)b : nbins + s));
-      do { b++; bend32 = offsets[b + 1]; } while (e >= bend32);
-      rs32 = e;
+      acc.store_raw(run_rec(raw, rec));
+      b++;
+      bend32 = bnext;
+      while (e >= bend32) {  // empty buckets
+        b++;
+        bend32 = offsets[b + 1];
+      }
+      rec = b;
       acc.set_inf();
     }
+    bnext = offsets[b + 2 <= nbins ? b + 2 : nbins];
     const uint32_t xw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
     const uint32_t yw[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
-    const bool negy = (v & 0x80000000u) != 0;
-    if (e + 1 < end32) {
-      const uint4* pn = reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(vn & KGS_DIAG_GATHER_MASK));
-      a0 = pn[0]; a1 = pn[1]; a2 = pn[2]; a3 = pn[3];
-      v = vn;
-      if (e + 2 < end32) vn = sorted[e + 2];
-    }
-    acc.add_aff(xw, yw, negy);
+    acc.add_aff(xw, yw, (v & 0x80000000u) != 0);
+    a0 = n0; a1 = n1; a2 = n2; a3 = n3;
+    v = vn;
+    vn = vnn;
   }
-  acc.store_raw(run_rec(raw, rs32 == offsets[b] ? (uint64_t)b : nbins + s));
+  acc.store_raw(run_rec(raw, rec));
 #ifdef KGS_DIAG_CLOCK
   if (threadIdx.x == 0 && blockIdx.x < KGS_CLK_BLOCKS) {
     const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
