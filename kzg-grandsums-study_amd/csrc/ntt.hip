@@ -279,10 +279,10 @@ __device__ __forceinline__ void bfly_pair_triv(fr* x, int r0, int r1, int dist) 
   x[r1 + dist] = fr::sub_lazy(a1, b1);
 }
 template <bool DIT>
-__device__ __forceinline__ void bfly_pair_x2(fr* x, int r0, int r1, int dist, const uint32_t* w0, const uint32_t* w1) {
+__device__ __forceinline__ void bfly_pair_x2(fr* x, int r0, int r1, int dist, const fr& w0, const fr& w1) {
   if (DIT) {
     fr b0, b1;
-    fr::mul_nored_x2(x[r0 + dist], fr::load(w0), x[r1 + dist], fr::load(w1), b0, b1);
+    fr::mul_nored_x2(x[r0 + dist], w0, x[r1 + dist], w1, b0, b1);
     const fr a0 = x[r0], a1 = x[r1];
     x[r0] = fr::add_lazy(a0, b0);
     x[r0 + dist] = fr::sub_lazy(a0, b0);
@@ -292,7 +292,7 @@ __device__ __forceinline__ void bfly_pair_x2(fr* x, int r0, int r1, int dist, co
     const fr d0 = fr::sub_2p(x[r0], x[r0 + dist]), d1 = fr::sub_2p(x[r1], x[r1 + dist]);
     x[r0] = fr::add_lazy(x[r0], x[r0 + dist]);
     x[r1] = fr::add_lazy(x[r1], x[r1 + dist]);
-    fr::mul_nored_x2(d0, fr::load(w0), d1, fr::load(w1), x[r0 + dist], x[r1 + dist]);
+    fr::mul_nored_x2(d0, w0, d1, w1, x[r0 + dist], x[r1 + dist]);
   }
 }
 // one register round of R stages of a pass on the 2^R elements j = jb + js * r (r < 2^R) of column
@@ -315,37 +315,61 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
     for (int r = 0; r < (1 << R); r++)
       x[r] = GIN ? ntt_load<DIT>(io, lds_idx(col, jb + js * r, K, logd)) : lds_ld(lds, (jb + js * r) * lb + cl);
   }
-#pragma unroll
-  for (int k = 0; k < R; k++) {
-    const int kp = kp0 + k;                                 // stage within the pass
-    const int logh = DIT ? logd + kp : logd + K - 1 - kp;   // half-distance h = 2^logh
-    const int dist = DIT ? 1 << k : 1 << (R - 1 - k);       // register distance
 #ifndef KGS_NTT_SINGLE
-    if constexpr (R >= 2) {
-      // Butterflies two at a time (q, q + half), their products interleaved (fr::mul_nored_x2; four at a
-      // time, fr::mul_nored_x4 at 232 VGPRs, measured 1.25x slower: profiles/r03/ntt_x2_x4.txt). A pair
-      // whose twiddles are all w^0 = 1 across the wave (low stages of the contiguous pass, where t depends
-      // on the register index only) skips its products; otherwise a lane with t == 0 multiplies by
-      // tw[h] = 1 (a product in [0, 2p) congruent to its input: same canonical output).
-      constexpr int half = 1 << (R - 2);
-      const uint32_t hm = (1u << logh) - 1;
-#define KGS_RR(q) ((((q) / dist) * 2 * dist) + ((q) % dist))
-#define KGS_T(q) (lds_idx(col, jb + js * KGS_RR(q), K, logd) & hm)
-      {
+  if constexpr (R >= 2) {
+    // Butterflies two at a time (q, q + half), their products interleaved (fr::mul_nored_x2; four at a
+    // time, fr::mul_nored_x4 at 232 VGPRs, measured 1.25x slower: profiles/r03/ntt_x2_x4.txt). A pair
+    // whose twiddles are all w^0 = 1 across the wave (low stages of the contiguous pass, where t depends
+    // on the register index only) skips its products; otherwise a lane with t == 0 multiplies by
+    // tw[h] = 1 (a product in [0, 2p) congruent to its input: same canonical output). The twiddles of
+    // the next (stage, pair) step are loaded before the current step's butterflies: each step is its
+    // own basic block (the uniform w^0 branch), so the compiler issued every twiddle load right before
+    // its product and waited on it there.
+    constexpr int half = 1 << (R - 2);
+    constexpr int NSTEP = R * half;
+    uint32_t tw0[NSTEP], tw1[NSTEP];  // twiddle indices (stage table offset + t) of each step
+    bool triv[NSTEP];
 #pragma unroll
-        for (int qa = 0; qa < half; qa++) {
-          const uint32_t t0 = KGS_T(qa), t1 = KGS_T(qa + half);
-          if (__all(t0 == 0 && t1 == 0))
-            bfly_pair_triv(x, KGS_RR(qa), KGS_RR(qa + half), dist);
-          else
-            bfly_pair_x2<DIT>(x, KGS_RR(qa), KGS_RR(qa + half), dist, tw + 8 * (hm + 1 + t0), tw + 8 * (hm + 1 + t1));
-        }
+    for (int k = 0; k < R; k++) {
+      const int kp = kp0 + k;
+      const int logh = DIT ? logd + kp : logd + K - 1 - kp;
+      const int dist = DIT ? 1 << k : 1 << (R - 1 - k);
+      const uint32_t hm = (1u << logh) - 1;
+#pragma unroll
+      for (int qa = 0; qa < half; qa++) {
+        const int r0 = ((qa / dist) * 2 * dist) + (qa % dist), r1 = (((qa + half) / dist) * 2 * dist) + ((qa + half) % dist);
+        const uint32_t t0 = lds_idx(col, jb + js * r0, K, logd) & hm, t1 = lds_idx(col, jb + js * r1, K, logd) & hm;
+        tw0[k * half + qa] = hm + 1 + t0;
+        tw1[k * half + qa] = hm + 1 + t1;
+        triv[k * half + qa] = __all(t0 == 0 && t1 == 0);
       }
-#undef KGS_T
-#undef KGS_RR
-    } else
+    }
+    fr wa = fr::load(tw + 8 * tw0[0]), wb = fr::load(tw + 8 * tw1[0]);
+#pragma unroll
+    for (int st = 0; st < NSTEP; st++) {
+      const int k = st / half, qa = st % half;
+      const int dist = DIT ? 1 << k : 1 << (R - 1 - k);
+      const int r0 = ((qa / dist) * 2 * dist) + (qa % dist), r1 = (((qa + half) / dist) * 2 * dist) + ((qa + half) % dist);
+      fr na, nb;
+      if (st + 1 < NSTEP) {
+        na = fr::load(tw + 8 * tw0[st + 1]);
+        nb = fr::load(tw + 8 * tw1[st + 1]);
+      }
+      if (triv[st])
+        bfly_pair_triv(x, r0, r1, dist);
+      else
+        bfly_pair_x2<DIT>(x, r0, r1, dist, wa, wb);
+      wa = na;
+      wb = nb;
+    }
+  } else
 #endif
-    {
+  {
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+      const int kp = kp0 + k;                                 // stage within the pass
+      const int logh = DIT ? logd + kp : logd + K - 1 - kp;   // half-distance h = 2^logh
+      const int dist = DIT ? 1 << k : 1 << (R - 1 - k);       // register distance
 #pragma unroll
       for (int q = 0; q < (1 << (R - 1)); q++) {
         const int r = ((q / dist) * 2 * dist) + (q % dist);
