@@ -11,6 +11,7 @@
 // Knobs: KGS_JS_CONTEXTS = contexts per device (default 8: with 16 concurrent calls, 8 contexts
 // reach 82 proofs/s at n = 2^20 against 78.5 with 4, profiles/r02/js_adaptive_lanes.txt), KGS_DEVICES = comma-separated device list (default: every visible device),
 // KGS_JS_SHARD_RANKS / KGS_JS_SHARD_MIN_NBITS = one large proof over several GPUs (below).
+const fs = require("fs");
 const path = require("path");
 const { contiguous } = require("./bigbuffer");
 
@@ -109,7 +110,17 @@ async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT) {
     if (selT) selT = contiguous(selT);
     if (shardRanks() >= 2 && nBits >= shardMinBits()) return proveSharded(kind, key, nBits, evalsF, evalsT, selF, selT);
     return withContext(async slot => {
-        await load().srsLoadPtau(slot.ctx, key, nBits);
+        // the SRS load is an async job (a libuv thread round trip) even when libkgs finds its tables
+        // already resident; skip it when this context loaded the same file (same real path, size and
+        // mtime — the identity libkgs checks, so a rewritten ptau is still re-read) for >= nBits
+        const st = fs.statSync(key, { bigint: true });
+        const id = `${fs.realpathSync(key)}#${st.size}#${st.mtimeNs}`;
+        if (slot.srsId !== id || slot.srsBits < nBits) {
+            slot.srsId = null;
+            await load().srsLoadPtau(slot.ctx, key, nBits);
+            slot.srsId = id;
+            slot.srsBits = nBits;
+        }
         setLanes(slot);
         const res = await load().prove(slot.ctx, kind, nBits, evalsF, evalsT, selF, selT);
         // diagnostics of the last call (time inside libkgs; kgs_last_timing rounds / copy / prover / write-back)
