@@ -1,7 +1,8 @@
 // Test driver used by tests/test_js_dropin.py: read {ptau, cases:[{kind, F:[hex], T:[hex], selF, selT}]}
 // from argv[2], run the drop-in provers, print {proofs:[{commitments:{k:hex}, evaluations:{k:hex}, montF:[hex]}]}.
 // With spec.concurrent every case is started at once (Promise.all), as independent reference calls
-// would be (src/grandsum/mset_eq_kzg_prover.js:12 is an independent async function per call).
+// would be (src/grandsum/mset_eq_kzg_prover.js:12 is an independent async function per call). A case
+// with replacePtau first copies that file over spec.ptau (a ptau rewritten between two calls).
 const fs = require("fs");
 const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_grandproduct_prover,
         lookup_kzg_grandsum_prover, mset_eq_kzg_grandsum_verifier, mset_eq_kzg_grandproduct_verifier,
@@ -13,6 +14,7 @@ const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_
     const hex = b => Buffer.from(b).toString("hex");
     const ev = h => new Evaluations(new Uint8Array(Buffer.from(h, "hex")), curve);
     const one = async c => {
+        if (c.replacePtau) fs.copyFileSync(c.replacePtau, spec.ptau);
         const F = c.F.map(ev), T = c.T.map(ev);
         const fn = { grandsum: mset_eq_kzg_grandsum_prover, grandproduct: mset_eq_kzg_grandproduct_prover,
                      lookup: lookup_kzg_grandsum_prover }[c.kind];

@@ -426,3 +426,28 @@ def test_js_prover_log_lines(tmp_path):
     assert out.returncode == 0, out.stderr[-2000:]
     assert "[WARN] The selection buffers are all zeros. The argument is trivially satisfied." in out.stderr
     assert "[INFO]" not in out.stderr
+
+
+@pytest.mark.gpu
+def test_js_rewritten_ptau_is_reread(tmp_path):
+    # the JS backend skips the SRS load when its context already holds the same file; a ptau rewritten
+    # at the same path (new mtime) between two calls must still be re-read, as the reference re-reads it
+    from oracle import ptau as opt
+    tau2 = (common.tau() + 12345) % common.R
+    path, other = str(tmp_path / "p.ptau"), str(tmp_path / "p2.ptau")
+    opt.write_synthetic_ptau(path, 6, common.tau())
+    opt.write_synthetic_ptau(other, 6, tau2)
+    Fs, Ts, _, _ = common.make_inputs(77, 4, 1, False)
+    case = {"kind": "grandsum", "F": [Fs[0].hex()], "T": [Ts[0].hex()], "selF": None, "selT": None}
+    spec = tmp_path / "spec.json"
+    spec.write_text(json.dumps({"ptau": path, "cases": [case, dict(case), dict(case, replacePtau=other), dict(case)]}))
+    out = json.loads(subprocess.check_output([NODE, os.path.join(JS, "test", "prove_from_json.js"), str(spec)],
+                                             timeout=300, env=dict(os.environ, KGS_JS_CONTEXTS="1")))
+    expect = []
+    for t in (common.tau(), tau2):
+        pr = P.prove("grandsum", P.SRS(other if t == tau2 else common.oracle_ptau(6), t), P.EvalBuffer(Fs[0]),
+                     P.EvalBuffer(Ts[0]))
+        expect.append({k: v.hex() for k, v in pr["commitments"].items()})
+    got = [p["commitments"] for p in out["proofs"]]
+    assert got[0] == expect[0] and got[1] == expect[0]
+    assert got[2] == expect[1] and got[3] == expect[1]
