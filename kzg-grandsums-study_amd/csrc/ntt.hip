@@ -350,11 +350,8 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
       const int k = st / half, qa = st % half;
       const int dist = DIT ? 1 << k : 1 << (R - 1 - k);
       const int r0 = ((qa / dist) * 2 * dist) + (qa % dist), r1 = (((qa + half) / dist) * 2 * dist) + ((qa + half) % dist);
-      fr na, nb;
-      if (st + 1 < NSTEP) {
-        na = fr::load(tw + 8 * tw0[st + 1]);
-        nb = fr::load(tw + 8 * tw1[st + 1]);
-      }
+      const int nx = st + 1 < NSTEP ? st + 1 : st;  // the last step reloads its own twiddles (unused)
+      const fr na = fr::load(tw + 8 * tw0[nx]), nb = fr::load(tw + 8 * tw1[nx]);
       if (triv[st])
         bfly_pair_triv(x, r0, r1, dist);
       else
