@@ -39,6 +39,8 @@ extern "C" {
 #define KGS_E_IO (-6)              /* ptau read/write failure (binfileutils / ptau_utils.js:3-24) */
 #define KGS_E_SRS (-7)             /* "The Powers of Tau file is not sufficiently large ..." (prover.js:79-81) */
 #define KGS_E_COMM (-8)            /* the shard all-gather callback reported a failure */
+#define KGS_E_RANGE (-9)           /* reference-quirks mode only: "offset is out of bounds", the V8 RangeError the
+                                      reference's divZh throws for a zero quotient (polynomial.js:857,884) */
 
 #define KGS_GRANDSUM 0
 #define KGS_GRANDPRODUCT 1
@@ -126,6 +128,22 @@ int kgs_ctx_set_group(kgs_ctx_t* ctx, kgs_group_t* g, int rank);
  * (single-proof latency -3 %, selected-vector 2^22 k=4 -7 %). Use 1 when several contexts already
  * keep the GPU busy with independent proofs (throughput). */
 int kgs_ctx_set_msm_lanes(kgs_ctx_t* ctx, int lanes);
+
+/* Reference-quirks mode (default off; a new context starts with the value of the environment variable
+ * KGS_REFERENCE_QUIRKS, "1" = on). Off, the prover returns a valid proof for every valid multiset. On,
+ * it reproduces what the reference does on the degenerate inputs where the reference does not
+ * compute the mathematical quotient (DESIGN.md §4 "Reference quirks"):
+ *   - an operand of degree 1 <= d < n/2 (F, T, S/Z, selF, selT — e.g. F[i] = w^i): the reference's
+ *     Polynomial.multiply evaluates it on the wrong points (polynomial.js:352-376 vs
+ *     evaluations.js:12-18); the reference's quotient chain is then replayed on the GPU with the
+ *     reference's buffer sizes and buffer sharing, and the prover fails where the reference fails
+ *     ("Polynomial is not divisible", "Polynomial does not divide") or returns the proof it returns;
+ *   - a zero quotient (e.g. F == T element by element): KGS_E_RANGE "offset is out of bounds".
+ * Only the two reference arguments are affected (KGS_LOOKUP has no reference behaviour to follow) and
+ * only the single-GPU prover (a context attached to a group fails with KGS_E_ARG). The replay
+ * reproduces transforms of up to 2^26 points (the reference's own need n^2 points for a degree-1
+ * operand); beyond that it fails with KGS_E_ARG. */
+int kgs_ctx_set_reference_quirks(kgs_ctx_t* ctx, int on);
 
 /* Load a .ptau file (binfileutils layout, sections 1-3) and make the first 2^(nbits_max+1) G1
  * points device-resident, together with the MSM window tables and the NTT tables for domains

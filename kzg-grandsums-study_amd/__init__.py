@@ -39,6 +39,20 @@ class KgsError(RuntimeError):
         self.code = code
 
 
+KGS_E_RANGE = -9
+
+
+class RangeError(ValueError):
+    """What the reference's JavaScript throws as a RangeError ("offset is out of bounds": its divZh on a
+    zero quotient, polynomial.js:857,884) — raised in reference-quirks mode only (include/kgs.h
+    kgs_ctx_set_reference_quirks)."""
+
+
+def _semantic(e):
+    """KgsError from the library -> the exception the reference's prover would throw."""
+    return RangeError(str(e)) if e.code == KGS_E_RANGE else ValueError(str(e))
+
+
 def lib():
     """Load lib/libkgs.so (raises if it is missing: the HIP path is the only path)."""
     global _lib
@@ -94,6 +108,7 @@ def lib():
                                       c_u8p]
         L.kgs_ctx_set_shard.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.kgs_ctx_set_msm_lanes.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.kgs_ctx_set_reference_quirks.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.kgs_shard_range.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_uint64)]
         L.kgs_msm_combine.argtypes = [c_u8p, ctypes.c_int, ctypes.c_int, c_u8p]
@@ -349,6 +364,11 @@ class Context:
     def handle(self):
         return self._h
 
+    def set_reference_quirks(self, on):
+        """Reference-quirks mode (kgs_ctx_set_reference_quirks; default: env KGS_REFERENCE_QUIRKS == "1"):
+        reproduce the reference's failures on degenerate inputs instead of proving them."""
+        _check(lib().kgs_ctx_set_reference_quirks(self._h, 1 if on else 0))
+
     def set_msm_lanes(self, lanes):
         """1 or 2 HIP streams for the independent MSMs of a prover round (kgs_ctx_set_msm_lanes)."""
         _check(lib().kgs_ctx_set_msm_lanes(self._h, lanes))
@@ -387,13 +407,13 @@ class Context:
             _check(lib().kgs_srs_load_ptau(self._h, os.fsencode(path), nbits_max))
         else:
             _check(lib().kgs_srs_load_ptau_slice(self._h, os.fsencode(path), nbits_max, int(slice[0]), int(slice[1])))
+        self._srs = (path, nbits_max, slice)
 
     def srs_slice_info(self):
         """(rank, world, window-table bytes) of the resident SRS (world 1: the whole prefix)"""
         r, w, b = ctypes.c_int(), ctypes.c_int(), ctypes.c_uint64()
         _check(lib().kgs_srs_slice_info(self._h, ctypes.byref(r), ctypes.byref(w), ctypes.byref(b)))
         return r.value, w.value, b.value
-        self._srs = (path, nbits_max)
 
     def srs_info(self):
         p, c = ctypes.c_int(), ctypes.c_int()
@@ -589,6 +609,8 @@ def _prover(kind, pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None
                      f"  Selectors: {'Yes' if is_selected else 'No'}", "-------------------------------------"):
             log.info(line)
     ctx = _context(device)
+    # the drop-in functions follow the environment on every call (contexts are cached per device)
+    ctx.set_reference_quirks(os.environ.get("KGS_REFERENCE_QUIRKS") == "1")
     # only the 2^(nbits+1) points this proof commits with (prover.js:83-85); grow-only device cache
     ctx.load_ptau(pTauFilename, nbits)
     coms, evs, mf, mt = ctx.prove(kind, nbits, [e.eval for e in evalsFs], [e.eval for e in evalsTs],
@@ -734,7 +756,7 @@ def grandsum_prover(pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=No
     try:
         return _prover(GRANDSUM, pTauFilename, evalsFs, evalsTs, evalsSelF, evalsSelT, device)
     except KgsError as e:
-        raise ValueError(str(e)) from e
+        raise _semantic(e) from e
 
 
 def grandproduct_prover(pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, device=0):
@@ -742,7 +764,7 @@ def grandproduct_prover(pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSel
     try:
         return _prover(GRANDPRODUCT, pTauFilename, evalsFs, evalsTs, evalsSelF, evalsSelT, device)
     except KgsError as e:
-        raise ValueError(str(e)) from e
+        raise _semantic(e) from e
 
 
 def _verifier(kind, pTauFilename, proof, nBits):
@@ -788,7 +810,7 @@ def lookup_prover(pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsMulT=None
     try:
         return _prover(LOOKUP, pTauFilename, evalsFs, evalsTs, evalsSelF, evalsMulT, device)
     except KgsError as e:
-        raise ValueError(str(e)) from e
+        raise _semantic(e) from e
 
 
 def lookup_verifier(pTauFilename, proof, nBits):

@@ -179,6 +179,7 @@ struct kgs_ctx {
   std::vector<hipEvent_t> ev_in;  // kgs_prove: one per input vector DMA'd on the copy stream
   MsmWork mw2;
   int msm_lanes = 2;  // kgs_ctx_set_msm_lanes
+  bool ref_quirks = false;  // kgs_ctx_set_reference_quirks (ref_quirks.cpp)
   uint64_t msm_nseg_max = 0;
   // domain tables (M = 2^logM; shared) and this context's views of them
   std::shared_ptr<DomainTables> dom;
@@ -317,8 +318,18 @@ namespace kgsi {
 void ensure_domain(kgs_ctx& c, int logM);
 uint32_t* get_nxm1(kgs_ctx& c, int nbits, int lcs);
 void intt_nat(kgs_ctx& c, uint32_t* out, const uint32_t* in, int logm, hipStream_t st = nullptr);
-void coset_fwd(kgs_ctx& c, uint32_t* out, const uint32_t* in, uint64_t len, int lcs);
-void coset_inv(kgs_ctx& c, uint32_t* out, const uint32_t* in, int lcs);
+// coefficients (len <= 2^lcs) -> coset evaluations p(g w^i), bit-reversed order
+void coset_fwd(kgs_ctx& c, uint32_t* out, const uint32_t* in, uint64_t len, int lcs, hipStream_t st = nullptr);
+// bit-reversed coset evaluations ALREADY SCALED BY 1/2^lcs -> natural coefficients (in place allowed);
+// the quotient takes its 1/cs from the Z_H scalars and get_nxm1's table
+void coset_inv_prescaled(kgs_ctx& c, uint32_t* out, const uint32_t* in, int lcs);
+
+// reference-quirks mode (ref_quirks.cpp; kgs_ctx_set_reference_quirks)
+bool ref_quirks_needed(kgs_ctx& c, uint64_t n, const std::vector<const uint32_t*>& ops);
+bool ref_quotient_is_zero(kgs_ctx& c, const uint32_t* Q, uint64_t qlen);
+uint32_t* ref_quirks_quotient(kgs_ctx& c, bool gs, bool sel, bool lookup, int nbits, const Fr& alpha, const Fr& gamma,
+                              const uint32_t* dF, const uint32_t* dT, const uint32_t* dS, const uint32_t* dSF,
+                              const uint32_t* dST, uint64_t& qlen, uint32_t*& fmut);
 
 // MSM commitment: device Pippenger -> c bit-sum points T_k (this rank's partial, pinned host)
 struct Commit {
@@ -397,7 +408,7 @@ struct R5 {
 };
 R5 round5_terms(bool gs, bool sel, int k, int nbits, const Fr& alpha, const Fr& beta, const Fr& gamma, const Fr& v,
                 const Fr& xi, const std::vector<Fr>& fx, const std::vector<Fr>& tx, const Fr& sFx, const Fr& sTx,
-                const Fr& sxiw, bool lookup);
+                const Fr& sxiw, bool lookup, const Fr* fxi_override = nullptr);
 
 void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out);
 // the distributed prover (prover_dist.cpp): same inputs and outputs as prove_impl on every rank

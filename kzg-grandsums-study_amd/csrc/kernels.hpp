@@ -84,6 +84,12 @@ void launch_from_mont(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_
 void launch_nxm1(hipStream_t st, uint32_t* out, const uint32_t* tw, uint64_t halfM, const uint32_t* gp,
                  const uint32_t* np, int lcs, uint64_t wstride);
 constexpr uint64_t EVAL_TILE = 2048;
+// reference-quirks mode (prover.cpp ref_quirks_*): degree, the reference's multiply/shiftOmega
+// pointwise step on its own evaluation domains, divZh in place
+void launch_degree(hipStream_t st, uint32_t* out, const uint32_t* a, uint64_t len);
+void launch_ref_gather_mul(hipStream_t st, uint32_t* out, const uint32_t* a, int loga, const uint32_t* b, int logb,
+                           uint64_t N, uint64_t rot);
+void launch_ref_divzh(hipStream_t st, uint32_t* c, uint64_t n, uint32_t ext, uint32_t* flag);
 
 // dist.hip (the distributed prover's rank-local kernels; layouts in prover_dist.cpp)
 void launch_gather_e(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t N, int W, int r, bool to_mont);

@@ -605,4 +605,70 @@ void launch_nxm1(hipStream_t st, uint32_t* out, const uint32_t* tw, uint64_t hal
   hipLaunchKernelGGL(k_nxm1, dim3(nb(1ull << lcs)), dim3(256), 0, st, out, tw, halfM, gp, np, lcs, wstride);
 }
 
+
+// ---------------------------------------------------------------------------- reference-quirks mode
+// (kgs_ctx_set_reference_quirks; prover.cpp ref_quirks_quotient). Not on the default path: these
+// kernels replay the reference's own `multiply` / `shiftOmega` / `divZh` buffer semantics on the GPU.
+
+// Polynomial.degree (polynomial.js:212-226): *out = max(*out, highest index i > 0 with a[i] != 0).
+// One atomic per wave (wave-wide max first); *out is zeroed by the caller.
+__global__ void k_degree(uint32_t* __restrict__ out, const uint32_t* __restrict__ a, uint64_t len) {
+  KGS_AUX_PRIO();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t d = 0;
+  if (i > 0 && i < len) {
+    const uint4 x = *(const uint4*)(a + 8 * i);
+    const uint4 y = *(const uint4*)(a + 8 * i + 4);
+    if (x.x | x.y | x.z | x.w | y.x | y.y | y.z | y.w) d = (uint32_t)i;
+  }
+  for (int o = 32; o > 0; o >>= 1) d = max(d, (uint32_t)__shfl_xor((int)d, o));
+  if ((threadIdx.x & 63) == 0 && d) atomicMax(out, d);
+}
+void launch_degree(hipStream_t st, uint32_t* out, const uint32_t* a, uint64_t len) {
+  if (len > 1) hipLaunchKernelGGL(k_degree, dim3(nb(len)), dim3(256), 0, st, out, a, len);
+}
+
+// The pointwise step of Polynomial.multiply / shiftOmega (polynomial.js:366-376, 378-393) on the
+// reference's own evaluation domains: a (2^loga points) and b (2^logb points) are DIF outputs
+// (bit-reversed order); out[i] = a_nat[(i + rot) mod 2^loga] * b_nat[i] for i < N, natural order
+// (b == nullptr: factor 1). The reference takes the FIRST N natural-order evaluations of each
+// operand's transform, whatever its size (evaluations.js:12-18).
+__global__ void k_ref_gather_mul(uint32_t* __restrict__ out, const uint32_t* __restrict__ a, int loga,
+                                 const uint32_t* __restrict__ b, int logb, uint64_t N, uint64_t rot) {
+  KGS_AUX_PRIO();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const uint32_t ia = (uint32_t)((i + rot) & ((1ull << loga) - 1));
+  fr x = fr::load(a + 8 * (uint64_t)brev(ia, loga));
+  if (b) x = x * fr::load(b + 8 * (uint64_t)brev((uint32_t)i, logb));
+  x.store(out + 8 * i);
+}
+void launch_ref_gather_mul(hipStream_t st, uint32_t* out, const uint32_t* a, int loga, const uint32_t* b, int logb,
+                           uint64_t N, uint64_t rot) {
+  hipLaunchKernelGGL(k_ref_gather_mul, dim3(nb(N)), dim3(256), 0, st, out, a, loga, b, logb, N, rot);
+}
+
+// Polynomial.divZh (polynomial.js:853-888) in place, one thread per residue r < n:
+//   c[r] = -c[r]; c[r + t n] = c[r + (t-1) n] - c[r + t n] for t < ext,
+// flagging "Polynomial is not divisible" for a nonzero value at i > n (ext - 1) - ext.
+__global__ void k_ref_divzh(uint32_t* __restrict__ c, uint64_t n, uint32_t ext, uint32_t* __restrict__ flag) {
+  KGS_AUX_PRIO();
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  fr acc = fr::zero() - fr::load(c + 8 * r);
+  acc.store(c + 8 * r);
+  const int64_t lim = (int64_t)n * (int64_t)(ext - 1) - (int64_t)ext;
+  bool bad = false;
+  for (uint32_t t = 1; t < ext; t++) {
+    const uint64_t i = r + (uint64_t)t * n;
+    acc = acc - fr::load(c + 8 * i);
+    acc.store(c + 8 * i);
+    if ((int64_t)i > lim && !acc.is_zero()) bad = true;
+  }
+  if (bad) *flag = 1;
+}
+void launch_ref_divzh(hipStream_t st, uint32_t* c, uint64_t n, uint32_t ext, uint32_t* flag) {
+  hipLaunchKernelGGL(k_ref_divzh, dim3(nb(n)), dim3(256), 0, st, c, n, ext, flag);
+}
+
 }  // namespace kgs

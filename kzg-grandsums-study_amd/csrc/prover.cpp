@@ -138,7 +138,7 @@ uint32_t* get_nxm1(kgs_ctx& c, int nbits, int lcs) {
   const uint64_t cs = 1ull << lcs;
   uint32_t* out = c.buf("nxm1_" + std::to_string(nbits) + "_" + std::to_string(lcs), 32 * cs);
   uint32_t* tmp = c.buf("nxm1_tmp", 32 * cs);
-  // 1/(n (x - 1)) / cs: the coset inverse NTT of the quotient (coset_inv) takes its 1/cs from here and
+  // 1/(n (x - 1)) / cs: the coset inverse NTT of the quotient (coset_inv_prescaled) takes its 1/cs from here and
   // from the Z_H scalars of round 3 instead of a product per element
   Fr consts[2] = {Fr::from_u64(5), Fr::from_u64(1ull << nbits) * Fr::from_u64(cs)};
   uint32_t* d = c.scal(consts, 2);
@@ -157,7 +157,7 @@ void intt_nat(kgs_ctx& c, uint32_t* out, const uint32_t* in, int logm, hipStream
   ntt_dit(st ? st : c.st, out, in, 0, logm, c.tw_inv, c.logM, nullptr, c.invm + 8 * logm);
 }
 // coefficients (len <= 2^lcs, natural) -> coset evaluations p(g w^i), bit-reversed order
-void coset_fwd(kgs_ctx& c, uint32_t* out, const uint32_t* in, uint64_t len, int lcs, hipStream_t st = nullptr) {
+void coset_fwd(kgs_ctx& c, uint32_t* out, const uint32_t* in, uint64_t len, int lcs, hipStream_t st) {
   ntt_dif(st ? st : c.st, out, in, len, lcs, c.coset_pow, c.tw_fwd, c.logM);
 }
 // bit-reversed coset evaluations, already scaled by 1/cs -> natural coefficients (in place allowed)
@@ -518,7 +518,7 @@ void run_lincomb(hipStream_t st, uint32_t* out, uint64_t n, const LcTerms& t) {
 // single-GPU and the distributed prover.
 R5 round5_terms(bool gs, bool sel, int k, int nbits, const Fr& alpha, const Fr& beta, const Fr& gamma, const Fr& v,
                 const Fr& xi, const std::vector<Fr>& fx, const std::vector<Fr>& tx, const Fr& sFx, const Fr& sTx,
-                const Fr& sxiw, bool lookup) {
+                const Fr& sxiw, bool lookup, const Fr* fxi_override) {
   const uint64_t n = 1ull << nbits;
   Fr xn = xi;
   for (int i = 0; i < nbits; i++) xn = xn.sqr();
@@ -529,6 +529,7 @@ R5 round5_terms(bool gs, bool sel, int k, int nbits, const Fr& alpha, const Fr& 
     fxi = fxi * beta + fx[i];
     if (gs) txi = txi * beta + tx[i];
   }
+  if (fxi_override) fxi = *fxi_override;
   const Fr one = Fr::one();
   Fr selBin = Fr::zero();  // alpha^3 selTBin + alpha^2 selFBin (a lookup has no selTBin term)
   if (sel) selBin = ((lookup ? Fr::zero() : (sTx - sTx.sqr()) * alpha) + (sFx - sFx.sqr())) * alpha * alpha;
@@ -583,6 +584,8 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   if (in.kind == KGS_LOOKUP && !in.sel_f)
     throw KgsError(KGS_E_ARG, "a lookup needs both selectors (sel_t holds the multiplicities)");
   if (c.group) {
+    if (c.ref_quirks && in.kind != KGS_LOOKUP)
+      throw KgsError(KGS_E_ARG, "reference-quirks mode runs on the single-GPU prover only");
     prove_dist_group(c, in, com_out, ev_out);
     return;
   }
@@ -825,7 +828,7 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   tr.add_commitment(com[iS].data());
   const Fr alpha = tr.challenge();
   const uint32_t rot = (uint32_t)(cs >> nbits);
-  const uint64_t qlen = (!gs && !sel) ? n - 1 : 2 * n - 2;  // deg Q + 1 bound
+  uint64_t qlen = (!gs && !sel) ? n - 1 : 2 * n - 2;  // deg Q + 1 bound
   Fr gn = Fr::from_u64(5).pow_u64(n);
   // alpha_t: weight of the selT-binary term (none for a lookup, whose selT holds multiplicities)
   // 1/Z_H on the two coset halves, times 1/cs (the scaling of the inverse transform below; nxm1 carries it too)
@@ -834,9 +837,9 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
               lk ? Fr::zero() : alpha};
   uint32_t* d_qs = c.scal(qs, 5);
   launch_divcheck(c.st, !gs, sel, flags + 1, Sev, fcomb, tcomb, in.sel_f, in.sel_t, d_qs, n);
-  uint32_t* Qc = c.buf("Qc", 32 * cs);
-  launch_quotient(c.st, !gs, sel, Qc, cosS, cosF, cosT, cosSF, cosST, nxm1, d_qs, lcs, rot);
-  coset_inv_prescaled(c, Qc, Qc, lcs);
+  const uint32_t* Qc = c.buf("Qc", 32 * cs);
+  launch_quotient(c.st, !gs, sel, (uint32_t*)Qc, cosS, cosF, cosT, cosSF, cosST, nxm1, d_qs, lcs, rot);
+  coset_inv_prescaled(c, (uint32_t*)Qc, Qc, lcs);
   check_launch();
   // latency mode: Q's 2n points over both MSM lanes (one lane's sort and tail overlap the other's
   // accumulation)
@@ -845,7 +848,37 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   slot += 2;
   HC(hipMemcpyAsync(h_flags, flags, 64, hipMemcpyDeviceToHost, c.st));
   c.sync();
-  if (h_flags[1]) throw KgsError(KGS_E_NOT_DIVISIBLE, "Polynomial is not divisible");
+  // Reference-quirks mode (ref_quirks.cpp): where the reference's own quotient chain does not compute
+  // the quotient (an operand of degree 1 <= d < n/2) it is replayed with the reference's buffer
+  // semantics and its Q replaces ours; otherwise the only difference is the reference's RangeError
+  // on a zero quotient (divZh, after its divisibility check).
+  const uint32_t* Fmut = nullptr;  // polF's buffer after the replay wrote into it (Q2), else nullptr
+  bool replayed = false;
+  if (c.ref_quirks && !lk) {
+    std::vector<const uint32_t*> ops = {polF, polT, Sc};
+    if (sel) {
+      ops.push_back(sFc);
+      ops.push_back(sTc);
+    }
+    if (ref_quirks_needed(c, n, ops)) {
+      uint32_t* fm_out = nullptr;
+      Qc = ref_quirks_quotient(c, gs, sel, lk, nbits, alpha, gamma, polF, polT, Sc, sFc, sTc, qlen, fm_out);
+      Fmut = fm_out;
+      replayed = true;
+      // multiExponentiation reads degree()+1 points of the reference's 2n-point PTau buffer
+      // (prover.js:83-84, polynomial.js:1106-1110); past it, ffjavascript's multiExpAffine gets fewer
+      // bases than scalars, which is not reproduced
+      if (qlen > 2 * n)
+        throw KgsError(KGS_E_ARG, "reference-quirks mode: the reference's Q has more coefficients than its 2n-point SRS buffer");
+      cQ = commit_launch_split(c, Qc, qlen, qlen / 2, slot);
+      slot += 2;
+      c.sync();
+    }
+  }
+  if (!replayed) {
+    if (h_flags[1]) throw KgsError(KGS_E_NOT_DIVISIBLE, "Polynomial is not divisible");
+    if (c.ref_quirks && !lk && ref_quotient_is_zero(c, Qc, qlen)) throw KgsError(KGS_E_RANGE, "offset is out of bounds");
+  }
   const int iQ = ci;
   commit_finish(c, cQ, com[ci++].data());
   lap(2);
@@ -858,6 +891,9 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   const Fr xiw = xi * w;
   std::vector<const uint32_t*> esrc;
   std::vector<uint64_t> elen;
+  // reference-quirks mode, polF's buffer shared and rewritten (Q2): the reference's later reads of polF
+  // see the new values — polFs[0] itself for one multiset, only polF.evaluate (prover.js:360) for vectors
+  if (Fmut && !vec) Fc[0] = (uint32_t*)Fmut;
   for (int i = 0; i < k; i++) {
     esrc.push_back(Fc[i]);
     elen.push_back(n);
@@ -870,6 +906,10 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     esrc.push_back(sFc);
     elen.push_back(n);
     esrc.push_back(sTc);
+    elen.push_back(n);
+  }
+  if (Fmut && vec) {
+    esrc.push_back(Fmut);
     elen.push_back(n);
   }
   EvalJob ej1 = eval_launch(c, esrc, elen, xi, 0);
@@ -888,6 +928,8 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     sFx = ev1[p++];
     sTx = ev1[p++];
   }
+  const bool fxi_set = Fmut && vec;
+  const Fr fxi_mut = fxi_set ? ev1[p++] : Fr::zero();
   std::vector<Fr> evals;  // proof order
   for (int i = 0; i < k; i++) {
     evals.push_back(fx[i]);
@@ -912,7 +954,8 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   }
   tr.add_scalar(sxiw);
   const Fr v = tr.challenge();
-  const R5 r5 = round5_terms(gs, sel, k, nbits, alpha, beta, gamma, v, xi, fx, tx, sFx, sTx, sxiw, lk);
+  const R5 r5 = round5_terms(gs, sel, k, nbits, alpha, beta, gamma, v, xi, fx, tx, sFx, sTx, sxiw, lk,
+                             fxi_set ? &fxi_mut : nullptr);
   LcTerms lw;
   for (const R5Term& t : r5.terms) {
     switch (t.id) {
@@ -1013,6 +1056,7 @@ int kgs_ctx_create(int device, kgs_ctx_t** out) {
     // the second MSM lane and the copy stream are created on first use: contexts that never need
     // them keep one stream (several in-flight contexts share the device's few hardware queues)
     c->d_scal = c->buf("scalars", kgs_ctx::SCAL_BYTES);
+    if (const char* e = getenv("KGS_REFERENCE_QUIRKS")) c->ref_quirks = e[0] == '1';
     c->ensure_pin(8 << 20);
     *out = c;
     return KGS_OK;
@@ -1049,6 +1093,14 @@ int kgs_device_count(int* count) {
   int n = 0;
   HC(hipGetDeviceCount(&n));
   *count = n;
+  API_END
+}
+
+int kgs_ctx_set_reference_quirks(kgs_ctx_t* ctx, int on) {
+  API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  CTX_LOCK(ctx);
+  ctx->ref_quirks = on != 0;
   API_END
 }
 

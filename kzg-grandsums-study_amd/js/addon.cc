@@ -444,7 +444,9 @@ static void job_complete(napi_env env, napi_status, void* data) {
   if (j->rc != KGS_OK) {
     napi_value msg, err, code;
     napi_create_string_utf8(env, j->err.c_str(), NAPI_AUTO_LENGTH, &msg);
-    napi_create_error(env, nullptr, msg, &err);
+    // the reference's divZh on a zero quotient throws V8's RangeError (reference-quirks mode only)
+    if (j->rc == KGS_E_RANGE) napi_create_range_error(env, nullptr, msg, &err);
+    else napi_create_error(env, nullptr, msg, &err);
     napi_create_int32(env, j->rc, &code);
     napi_set_named_property(env, err, "kgsCode", code);
     napi_reject_deferred(env, j->deferred, err);

@@ -5,10 +5,32 @@ Op-for-op restatement of the reference's `Polynomial` (src/polynomial/polynomial
 sizes and, for `multiply`, the degenerate-degree quirk of SURVEY.md Appendix C.1). Values are kept
 as standard-form Python ints; the byte representation (32 B LE Montgomery) is applied only at the
 proof boundary, which is value-identical to ffjavascript's in-memory Montgomery buffers.
+
+Two semantics (module flag QUIRKS, set per proof by `protocol.prove(..., quirks=...)`):
+  * QUIRKS = True (default): the reference exactly, including three behaviours that only show on
+    degenerate inputs (DESIGN.md §4 "Reference quirks"):
+      Q1 `multiply` sizes each operand's FFT from its DEGREE but `Evaluations.fromPolynomial` pads
+         from its buffer LENGTH (polynomial.js:352-376, evaluations.js:12-18): an operand of degree
+         d >= 1 with 2^ceil(log2(d+1)) < 2^ceil(log2(length)) is evaluated on the wrong points;
+      Q2 `add`/`sub` with a LONGER argument write into the argument's buffer and adopt it
+         (polynomial.js:276-350): the two objects then share one buffer, and later in-place
+         operations on either change both (lists are shared here exactly as buffers are there);
+      Q3 `divZh` copies degree()+1 coefficients into a buffer of 0 elements when the dividend's
+         degree is below the domain size (polynomial.js:857,884): V8's TypedArray `set` throws
+         "RangeError: offset is out of bounds" (a zero quotient).
+  * QUIRKS = False: the same operation sequence with exact products (both operands padded to the
+    product's domain), no buffer sharing and a zero quotient kept — the mathematical values the
+    MI355X prover computes in its default mode. On every non-degenerate input (all golden vectors)
+    both semantics give the identical proof.
 """
 from . import bn254 as bn
 
 R = bn.R
+QUIRKS = True
+
+
+class JSRangeError(ValueError):
+    """V8's RangeError from TypedArray.prototype.set (message as V8 prints it)."""
 
 
 def _clog2(x):
@@ -156,37 +178,45 @@ class Polynomial:
             res = (res * x + self.coef[i]) % R
         return res
 
-    # polynomial.js:276-312 (zero-extends; the aliasing of the longer buffer has no value effect)
+    # polynomial.js:276-312 / 314-350. Reference: when `other` is strictly longer the result is
+    # written into other's buffer and self adopts it (Q2); otherwise into self's buffer, in place.
+    def _addsub(self, other, sign, blinding):
+        L = max(self.length(), other.length())
+        a = self.coef + [0] * (L - self.length())
+        b = other.coef + [0] * (L - other.length())
+        if blinding is not None:
+            b = [x * blinding % R for x in b]
+        res = [(x + sign * y) % R for x, y in zip(a, b)]
+        if QUIRKS and other.length() > self.length():
+            other.coef[:] = res
+            self.coef = other.coef
+        elif self.length() == L:
+            self.coef[:] = res
+        else:
+            self.coef = res
+        return self
+
     def add(self, other, blinding=None):
-        L = max(self.length(), other.length())
-        a = self.coef + [0] * (L - self.length())
-        b = other.coef + [0] * (L - other.length())
-        if blinding is not None:
-            b = [x * blinding % R for x in b]
-        self.coef = [(x + y) % R for x, y in zip(a, b)]
-        return self
+        return self._addsub(other, 1, blinding)
 
-    # polynomial.js:314-350
     def sub(self, other, blinding=None):
-        L = max(self.length(), other.length())
-        a = self.coef + [0] * (L - self.length())
-        b = other.coef + [0] * (L - other.length())
-        if blinding is not None:
-            b = [x * blinding % R for x in b]
-        self.coef = [(x - y) % R for x, y in zip(a, b)]
-        return self
+        return self._addsub(other, -1, blinding)
 
-    # polynomial.js:352-376 — sizes derived exactly as the reference does (Appendix C.1)
+    # polynomial.js:352-376 — sizes derived exactly as the reference does (Q1; Appendix C.1)
     def multiply(self, other):
         new_degree = self.degree() + other.degree()
         new_power = _clog2(new_degree + 1)
         new_length = 1 << new_power
-        power1 = _clog2(self.degree() + 1)
-        power2 = _clog2(other.degree() + 1)
-        factor1 = 1 << (new_power - power1)
-        factor2 = 1 << (new_power - power2)
-        e1 = Evaluations.from_polynomial(self, factor1).vals
-        e2 = Evaluations.from_polynomial(other, factor2).vals
+        if QUIRKS:
+            power1 = _clog2(self.degree() + 1)
+            power2 = _clog2(other.degree() + 1)
+            factor1 = 1 << (new_power - power1)
+            factor2 = 1 << (new_power - power2)
+            e1 = Evaluations.from_polynomial(self, factor1).vals
+            e2 = Evaluations.from_polynomial(other, factor2).vals
+        else:
+            e1 = ntt(self.coef[:new_length] + [0] * (new_length - min(new_length, self.length())))
+            e2 = ntt(other.coef[:new_length] + [0] * (new_length - min(new_length, other.length())))
         prod = [e1[i] * e2[i] % R for i in range(new_length)]
         self.coef = ntt(prod, True)
         return self
@@ -200,7 +230,7 @@ class Polynomial:
 
     # polynomial.js:395-406
     def mul_scalar(self, v):
-        self.coef = [c * v % R for c in self.coef]
+        self.coef[:] = [c * v % R for c in self.coef]
         return self
 
     # polynomial.js:408-422
@@ -267,6 +297,8 @@ class Polynomial:
             if i > n * (ext - 1) - ext and a != 0:
                 raise ValueError("Polynomial is not divisible")
         d = self.degree()
+        if QUIRKS and d + 1 > length:
+            raise JSRangeError("offset is out of bounds")  # Q3: Uint8Array(0).set(32 bytes)
         nb = [0] * length
         nb[:d + 1] = c[:d + 1]
         self.coef = nb

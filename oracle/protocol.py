@@ -18,7 +18,8 @@ group element (used to keep the pure-Python oracle fast; tests pin the two again
 """
 from . import bn254 as bn
 from .keccak import keccak256
-from .poly import Polynomial, Evaluations, batch_inverse
+from . import poly as OP
+from .poly import Polynomial, Evaluations, batch_inverse, JSRangeError  # noqa: F401
 from .ptau import PTau
 
 R = bn.R
@@ -190,12 +191,25 @@ def _grandproduct_Z(evF, evT, selF, selT, gamma):
     return Polynomial.from_evaluations(num)
 
 
-def prove(kind, srs, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, trace=None):
+def prove(kind, srs, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None, trace=None, quirks=None):
     """kind in {"grandsum", "grandproduct", "lookup"}; returns the proof dict (byte-level ffjs
-    encoding). "lookup" (test/lookup_kzg_grandsum.test.js:24-44, commented out in
+    encoding). quirks=True: the reference exactly (oracle/poly.py Q1-Q3: on degenerate inputs it
+    throws "Polynomial is not divisible" / "Polynomial does not divide" / JSRangeError where the
+    reference does); quirks=False: the same operations with exact values (the MI355X prover's
+    default mode). Default (None): True for the reference's two arguments, False for "lookup" (not a
+    reference prover: its restatement has no reference behaviour to follow on degenerate inputs). "lookup" (test/lookup_kzg_grandsum.test.js:24-44, commented out in
     the reference, so this restatement is parity-unpinned): the selected grand-sum with evalsSelT
     holding the table's multiplicities and no binary constraint on selT (prover.js:241-244 dropped)."""
     assert kind in ("grandsum", "grandproduct", "lookup")
+    saved = OP.QUIRKS
+    OP.QUIRKS = (kind != "lookup") if quirks is None else bool(quirks)
+    try:
+        return _prove(kind, srs, evalsFs, evalsTs, evalsSelF, evalsSelT, trace)
+    finally:
+        OP.QUIRKS = saved
+
+
+def _prove(kind, srs, evalsFs, evalsTs, evalsSelF, evalsSelT, trace):
     gs = kind != "grandproduct"
     lookup = kind == "lookup"
     evalsFs, evalsTs, selFv, selTv, is_selected, nbits = _check_inputs(

@@ -251,19 +251,27 @@ def test_error_paths(K):
 
 
 def test_trivial_identity_multiset(K):
-    """F == T: S == 0 (grand-sum) / Z == 1; commitments of zero polynomials are infinity."""
+    """F == T: S == 0 (grand-sum) / Z == 1; commitments of zero polynomials are infinity. The quotient
+    is zero, on which the reference's divZh throws V8's RangeError (oracle quirk Q3,
+    tests/test_gpu_quirks.py): the default mode proves it with the exact values (oracle quirks=False)."""
+    from oracle import poly as OP
     Fs, _, _, _ = common.make_inputs(8, 3, 1, False)
     srs = P.SRS(common.oracle_ptau(9), common.tau())
     for kind, fn in (("grandsum", K.grandsum_prover), ("grandproduct", K.grandproduct_prover)):
         got = fn(common.oracle_ptau(9), K.Evaluations(Fs[0]), K.Evaluations(Fs[0]))
-        exp = P.prove(kind, srs, P.EvalBuffer(Fs[0]), P.EvalBuffer(Fs[0]))
+        exp = P.prove(kind, srs, P.EvalBuffer(Fs[0]), P.EvalBuffer(Fs[0]), quirks=False)
         assert got == exp
+        with pytest.raises(OP.JSRangeError, match="offset is out of bounds"):
+            P.prove(kind, srs, P.EvalBuffer(Fs[0]), P.EvalBuffer(Fs[0]))
 
 
 def test_all_zero_selectors(K):
-    """selF = selT = 0 with F, T unrelated: trivially satisfied — the reference only warns "The
-    selection buffers are all zeros" (src/grandsum/mset_eq_kzg_prover.js:66-68) and proves; S = 0 and
-    Z = 1, so several commitments are of constant polynomials. Byte-exact vs the oracle, verified."""
+    """selF = selT = 0 with F, T unrelated: trivially satisfied — the reference warns "The selection
+    buffers are all zeros" (src/grandsum/mset_eq_kzg_prover.js:66-68); S = 0 and Z = 1, so several
+    commitments are of constant polynomials and the quotient is zero, on which the reference's divZh
+    then throws V8's RangeError (oracle quirk Q3). Default mode: byte-exact vs the oracle's exact values
+    (quirks=False), verified."""
+    from oracle import poly as OP
     ptau = common.oracle_ptau(9)
     srs = P.SRS(ptau, common.tau())
     Fs, _, _, _ = common.make_inputs(31, 4, 2, False)
@@ -274,9 +282,12 @@ def test_all_zero_selectors(K):
         got = fn(ptau, [K.Evaluations(x) for x in Fs], [K.Evaluations(x) for x in Ts],
                  K.Evaluations(zero), K.Evaluations(zero))
         exp = P.prove(kind, srs, [P.EvalBuffer(x) for x in Fs], [P.EvalBuffer(x) for x in Ts],
-                      P.EvalBuffer(zero), P.EvalBuffer(zero))
+                      P.EvalBuffer(zero), P.EvalBuffer(zero), quirks=False)
         assert got == exp
         assert vf(ptau, got, 4) is True
+        with pytest.raises(OP.JSRangeError, match="offset is out of bounds"):
+            P.prove(kind, srs, [P.EvalBuffer(x) for x in Fs], [P.EvalBuffer(x) for x in Ts],
+                    P.EvalBuffer(zero), P.EvalBuffer(zero))
 
 
 def _bary_eval(vals, nbits, x):
