@@ -101,3 +101,26 @@ def test_non_binary_selector_not_divisible(srs6, kind):
     with pytest.raises(ValueError, match="Polynomial is not divisible"):
         P.prove(kind, srs6, P.EvalBuffer(common.std_bytes(f)), P.EvalBuffer(common.std_bytes(f)),
                 P.EvalBuffer(common.mont_bytes(sel)), P.EvalBuffer(common.mont_bytes(sel)))
+
+
+def test_reference_quirks_on_degenerate_multisets(srs6):
+    """oracle/poly.py Q1-Q3: F = w^i (degree 1) makes the reference's multiply
+    mis-sized, F == T gives a zero quotient; the exact semantics prove both and the proofs verify."""
+    from oracle import poly as OP
+    nb, n = 3, 8
+    w = bn.FR_W[nb]
+    f = [pow(w, i, R) for i in range(n)]
+    rot = [f[-1]] + f[:-1]
+    cases = [("grandsum", f, rot, "Polynomial is not divisible"), ("grandproduct", f, rot, "Polynomial does not divide"),
+             ("grandsum", f, f, None), ("grandproduct", f, f, None)]
+    for kind, fv, tv, msg in cases:
+        def args():  # fresh buffers: the prover writes the Montgomery form back into them
+            return (kind, srs6, P.EvalBuffer(common.std_bytes(fv)), P.EvalBuffer(common.std_bytes(tv)))
+        if msg is None:
+            with pytest.raises(OP.JSRangeError, match="offset is out of bounds"):
+                P.prove(*args())
+        else:
+            with pytest.raises(ValueError, match=msg):
+                P.prove(*args())
+        proof = P.prove(*args(), quirks=False)
+        assert P.verify(kind, srs6.ptau, proof, nb, tau=common.tau())
