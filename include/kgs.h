@@ -97,7 +97,11 @@ int kgs_msm_combine(const uint8_t* T_all, int nparts, int c, uint8_t out_lem[64]
  * whole SRS (kgs_srs_load_ptau: the MSMs read it with a point stride) or only its slice
  * (kgs_srs_load_ptau_slice(ctx, path, nbits, rank, world): 1/world of the tables).
  * Transports:
- *   local : several contexts of ONE process (one host thread per rank; devices may differ)
+ *   local : several contexts of ONE process (one host thread per rank; devices may differ: attaching a
+ *           context, kgs_ctx_set_group, enables peer access between its device and every other attached
+ *           rank's device, and fails with KGS_E_COMM for a pair without peer access — the all-to-all
+ *           then copies device to device over xGMI; UNVERIFIED on more than one device: every run of
+ *           this build had one GPU, so all ranks shared a device)
  *   host  : any host all-gather callback (e.g. torch.distributed gloo); device data via the host
  *   rccl  : one process per GPU, RCCL over xGMI (rank 0 makes the id, the caller broadcasts it)
  * Failures:

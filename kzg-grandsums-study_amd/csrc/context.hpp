@@ -137,6 +137,9 @@ struct kgs_group {
   virtual void alltoall(int rank, struct kgs_ctx& c, hipStream_t st, const void* send, void* recv, size_t chunk) = 0;
   // a rank failed: unblock the others (they fail too instead of waiting forever)
   virtual void abort() {}
+  // a context on `device` becomes `rank` (kgs_ctx_set_group): transports that move device data
+  // between the ranks' devices directly prepare that here
+  virtual void attach(int rank, int device) { (void)rank; (void)device; }
   virtual void wait(hipStream_t st) {
     const hipError_t e = hipStreamSynchronize(st);
     if (e != hipSuccess) throw KgsError(KGS_E_HIP, std::string("HIP error: ") + hipGetErrorString(e) + " (stream sync)");
@@ -174,8 +177,12 @@ struct kgs_ctx {
   // between st and st2 (own work buffers), so one MSM's latency-bound tail overlaps the other's
   // bucket accumulation
   hipStream_t st2 = nullptr;
-  hipStream_t st_copy = nullptr;  // Montgomery write-back of the host-buffer boundary
-  hipEvent_t ev_fork = nullptr, ev_copy = nullptr, ev_copy2 = nullptr, ev_join = nullptr;
+  hipStream_t st_copy = nullptr;  // kgs_prove's input DMAs (vectors 1..)
+  // the Montgomery write-back (prover.js:147-148): its own stream, so that it never sits between
+  // the input DMAs on st_copy; each vector's D2H waits only for that vector's conversion
+  hipStream_t st_wb = nullptr;
+  std::vector<hipEvent_t> ev_wb;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::vector<hipEvent_t> ev_in;  // kgs_prove: one per input vector DMA'd on the copy stream
   MsmWork mw2;
   int msm_lanes = 2;  // kgs_ctx_set_msm_lanes
@@ -203,14 +210,15 @@ struct kgs_ctx {
     if (st) hipStreamSynchronize(st);
     if (st2) hipStreamSynchronize(st2);
     if (st_copy) hipStreamSynchronize(st_copy);
+    if (st_wb) hipStreamSynchronize(st_wb);
     for (auto& kv : pool) hipFree(kv.second.p);
     if (h_pin) hipHostFree(h_pin);
     if (h_io) hipHostFree(h_io);
     if (ev_fork) hipEventDestroy(ev_fork);
-    if (ev_copy) hipEventDestroy(ev_copy);
-    if (ev_copy2) hipEventDestroy(ev_copy2);
     if (ev_join) hipEventDestroy(ev_join);
     for (hipEvent_t e : ev_in) hipEventDestroy(e);
+    for (hipEvent_t e : ev_wb) hipEventDestroy(e);
+    if (st_wb) hipStreamDestroy(st_wb);
     if (st_copy) hipStreamDestroy(st_copy);
     if (st2) hipStreamDestroy(st2);
     if (st) hipStreamDestroy(st);
@@ -286,6 +294,7 @@ struct kgs_ctx {
     else HC(hipStreamSynchronize(st));
     if (st2) HC(hipStreamSynchronize(st2));
     if (st_copy) HC(hipStreamSynchronize(st_copy));
+    if (st_wb) HC(hipStreamSynchronize(st_wb));
   }
   void reset_staging() {
     sync();
@@ -389,7 +398,7 @@ struct ProveIn {
   std::vector<const uint32_t*> f_std, t_std;  // device, standard form
   const uint32_t *sel_f = nullptr, *sel_t = nullptr;  // device, Montgomery (nullptr: unselected)
   std::vector<uint8_t*> mont_f_out, mont_t_out;  // host outputs (may be empty)
-  std::function<void()> after_round1;             // called once round 1 is synchronised
+  std::function<void()> after_round1;             // called once round 1 is synchronised (write-back on st_wb)
   // kgs_prove: per input vector (F_i at 2i, T_i at 2i + 1, then selF, selT) an event the main stream
   // waits for before the vector's first kernel, or nullptr (already ordered on the main stream)
   std::vector<hipEvent_t> ready;

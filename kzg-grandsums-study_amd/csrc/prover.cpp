@@ -653,6 +653,23 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     if (in.input_issued) in.input_issued(v);
     if (v < in.ready.size() && in.ready[v]) HC(hipStreamWaitEvent(st, in.ready[v], 0));
   };
+  // Montgomery write-back (prover.js:147-148): vector v's D2H on the write-back stream right after
+  // its conversion on `st` (not after the round's MSMs, and never queued between input DMAs)
+  int nwb = 0;
+  auto write_back = [&](uint8_t* dst, const uint32_t* src, hipStream_t st) {
+    if (!dst) return;
+    if (!c.st_wb) HC(hipStreamCreateWithFlags(&c.st_wb, hipStreamNonBlocking));
+    if ((int)c.ev_wb.size() <= nwb) {
+      hipEvent_t e;
+      HC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c.ev_wb.push_back(e);
+    }
+    HC(hipEventRecord(c.ev_wb[nwb], st));
+    HC(hipStreamWaitEvent(c.st_wb, c.ev_wb[nwb], 0));
+    nwb++;
+    HC(hipMemcpyAsync(dst, src, E, hipMemcpyDeviceToHost, c.st_wb));
+  };
+  auto mont_out = [&](const std::vector<uint8_t*>& v, int i) -> uint8_t* { return v.empty() ? nullptr : v[i]; };
   std::vector<Commit> r1;
   int slot = 0;
   // With two MSM lanes (a proof alone on its context: the latency mode) each input vector's whole
@@ -665,10 +682,12 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     for (int i = 0; i < k; i++) {
       wait_input(2 * i, c.st);
       launch_to_mont(c.st, fm[i], in.f_std[i], n);
+      write_back(mont_out(in.mont_f_out, i), fm[i], c.st);
       intt_nat(c, Fc[i], fm[i], nbits);
       r1.push_back(commit_launch(c, Fc[i], n, slot++, 0));
       wait_input(2 * i + 1, c.st2);
       launch_to_mont(c.st2, tm[i], in.t_std[i], n);
+      write_back(mont_out(in.mont_t_out, i), tm[i], c.st2);
       intt_nat(c, Tc[i], tm[i], nbits, c.st2);
       r1.push_back(commit_launch(c, Tc[i], n, slot++, 1));
     }
@@ -677,34 +696,16 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     for (int i = 0; i < k; i++) {
       wait_input(2 * i, c.st);
       launch_to_mont(c.st, fm[i], in.f_std[i], n);
+      write_back(mont_out(in.mont_f_out, i), fm[i], c.st);
       wait_input(2 * i + 1, c.st);
       launch_to_mont(c.st, tm[i], in.t_std[i], n);
+      write_back(mont_out(in.mont_t_out, i), tm[i], c.st);
       intt_nat(c, Fc[i], fm[i], nbits);
       intt_nat(c, Tc[i], tm[i], nbits);
     }
     check_launch();
   }
-  // Montgomery write-back (prover.js:147-148) on the copy stream, overlapping round 1's MSMs;
-  // fm/tm are not written again before the round-1 sync
-  bool wb = false;
-  for (int i = 0; i < k; i++) wb |= !in.mont_f_out.empty() && (in.mont_f_out[i] || in.mont_t_out[i]);
-  if (wb) {
-    if (!c.st_copy) {
-      HC(hipStreamCreateWithFlags(&c.st_copy, hipStreamNonBlocking));
-      HC(hipEventCreateWithFlags(&c.ev_copy, hipEventDisableTiming));
-    }
-    HC(hipEventRecord(c.ev_copy, c.st));
-    HC(hipStreamWaitEvent(c.st_copy, c.ev_copy, 0));
-    if (piped) {  // the T_i conversions ran on lane 1
-      if (!c.ev_copy2) HC(hipEventCreateWithFlags(&c.ev_copy2, hipEventDisableTiming));
-      HC(hipEventRecord(c.ev_copy2, c.st2));
-      HC(hipStreamWaitEvent(c.st_copy, c.ev_copy2, 0));
-    }
-    for (int i = 0; i < k; i++) {
-      if (in.mont_f_out[i]) HC(hipMemcpyAsync(in.mont_f_out[i], fm[i], E, hipMemcpyDeviceToHost, c.st_copy));
-      if (in.mont_t_out[i]) HC(hipMemcpyAsync(in.mont_t_out[i], tm[i], E, hipMemcpyDeviceToHost, c.st_copy));
-    }
-  }
+  // fm/tm are not written again before the round-1 sync (the write-back reads them on st_wb)
   if (sel) {
     if (piped) {
       wait_input(2 * k, c.st);
@@ -731,8 +732,8 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
       r1.push_back(commit_launch(c, sTc, n, slot++, 1));
     }
   }
-  // round 1's commitments only: the Montgomery write-back on the copy stream keeps running under
-  // rounds 2-5 (in.after_round1's thread waits for it before copying to the caller)
+  // round 1's commitments only: the Montgomery write-back on st_wb keeps running under rounds 2-5
+  // (in.after_round1's thread waits for it before copying to the caller)
   HC(hipStreamSynchronize(c.st));
   if (c.st2) HC(hipStreamSynchronize(c.st2));
   if (in.after_round1) in.after_round1();
@@ -1420,6 +1421,7 @@ struct HostPins {
     if (ctx->st) hipStreamSynchronize(ctx->st);
     if (ctx->st2) hipStreamSynchronize(ctx->st2);
     if (ctx->st_copy) hipStreamSynchronize(ctx->st_copy);
+    if (ctx->st_wb) hipStreamSynchronize(ctx->st_wb);
     std::lock_guard<std::mutex> lk(g_pin_mu);
     for (void* p : mine) drop(p);
   }
@@ -1493,6 +1495,9 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
       HC(hipMemcpyAsync((uint8_t*)dsts[v] + o, in_jobs[v].dst + o, len, hipMemcpyHostToDevice, st));
     }
   };
+  // declared before the feeder: destroyed after it is joined, so streams are drained and buffers
+  // unpinned only once nothing can enqueue another DMA on them
+  HostPins pins(ctx);
   struct Feeder {  // the input-copy thread of vectors 1.. (joined on every exit path)
     std::thread t;
     std::mutex mu;
@@ -1504,7 +1509,6 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
     }
   } feeder;
   Range rin("kgs.host.input_copy");
-  HostPins pins(ctx);  // declared after the feeder: released only once every stream is drained
   bool direct = !ctx->group;
   for (size_t v = 0; direct && v < in_jobs.size(); v++) direct = pins.pin(in_jobs[v].src, E);
   if (!direct) pins.release_from(0);
@@ -1512,10 +1516,7 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
     // zero-copy: every input DMA'd straight from the caller's pinned buffer, one after the other on the
     // copy stream (not two streams at once: F_0 then arrives after one vector's transfer time instead
     // of sharing the link with T_0), each with the event its first kernel waits for
-    if (!ctx->st_copy) {
-      HC(hipStreamCreateWithFlags(&ctx->st_copy, hipStreamNonBlocking));
-      HC(hipEventCreateWithFlags(&ctx->ev_copy, hipEventDisableTiming));
-    }
+    if (!ctx->st_copy) HC(hipStreamCreateWithFlags(&ctx->st_copy, hipStreamNonBlocking));
     while (ctx->ev_in.size() < in_jobs.size()) {
       hipEvent_t e;
       HC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1537,10 +1538,7 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
     // waits for right before the vector's first kernel, so F_0's transform starts while the rest
     // are still in flight. (The Montgomery write-back later reuses the same pinned slots on the
     // copy stream, after these DMAs in stream order.)
-    if (!ctx->st_copy) {
-      HC(hipStreamCreateWithFlags(&ctx->st_copy, hipStreamNonBlocking));
-      HC(hipEventCreateWithFlags(&ctx->ev_copy, hipEventDisableTiming));
-    }
+    if (!ctx->st_copy) HC(hipStreamCreateWithFlags(&ctx->st_copy, hipStreamNonBlocking));
     while (ctx->ev_in.size() < in_jobs.size()) {
       hipEvent_t e;
       HC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1613,8 +1611,8 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   if (!out_jobs.empty())
     in.after_round1 = [&] {
       out_copy.t = std::thread([&, dev = ctx->device] {
-        // the device -> pinned write-back (copy stream) must be complete before the pinned -> caller copy
-        if (hipSetDevice(dev) != hipSuccess || hipStreamSynchronize(ctx->st_copy) != hipSuccess) {
+        // the device -> pinned write-back (st_wb) must be complete before the pinned -> caller copy
+        if (hipSetDevice(dev) != hipSuccess || (ctx->st_wb && hipStreamSynchronize(ctx->st_wb) != hipSuccess)) {
           out_copy.failed = true;
           return;
         }

@@ -55,8 +55,36 @@ struct LocalGroup : kgs_group {
   bool broken = false;
   std::vector<const void*> sp;
   std::vector<int> dev;
+  std::vector<int> attached;  // device of each attached rank (-1: none yet)
 
-  explicit LocalGroup(int w) : sp(w), dev(w) { world = w; }
+  explicit LocalGroup(int w) : sp(w), dev(w), attached(w, -1) { world = w; }
+
+  // `a` reads from / writes to `b`'s memory in the all-to-all (hipMemcpyPeerAsync): without peer
+  // access the runtime would stage the copy through the host, so a pair without it fails up front
+  static void enable_peer(int a, int b) {
+    int can = 0;
+    HC(hipDeviceCanAccessPeer(&can, a, b));
+    if (!can)
+      throw KgsError(KGS_E_COMM, "in-process rank group: device " + std::to_string(a) + " has no peer access to device " +
+                                     std::to_string(b) + " (hipDeviceCanAccessPeer); use one process per GPU (RCCL)");
+    int cur = 0;
+    HC(hipGetDevice(&cur));
+    HC(hipSetDevice(a));
+    const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+    (void)hipGetLastError();
+    HC(hipSetDevice(cur));
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+      throw KgsError(KGS_E_COMM, std::string("in-process rank group: hipDeviceEnablePeerAccess failed: ") + hipGetErrorString(e));
+  }
+  void attach(int rank, int device) override {
+    std::lock_guard<std::mutex> lk(mu);
+    for (int j = 0; j < world; j++)
+      if (j != rank && attached[j] >= 0 && attached[j] != device) {
+        enable_peer(device, attached[j]);
+        enable_peer(attached[j], device);
+      }
+    attached[rank] = device;
+  }
 
   void barrier() {
     std::unique_lock<std::mutex> lk(mu);
@@ -95,7 +123,7 @@ struct LocalGroup : kgs_group {
       uint8_t* dst = (uint8_t*)recv + (size_t)j * chunk;
       const uint8_t* src = (const uint8_t*)sp[j] + (size_t)rank * chunk;
       if (dev[j] == c.device) HC(hipMemcpyAsync(dst, src, chunk, hipMemcpyDeviceToDevice, st));
-      else HC(hipMemcpyPeerAsync(dst, c.device, src, dev[j], chunk, st));
+      else HC(hipMemcpyPeerAsync(dst, c.device, src, dev[j], chunk, st));  // peer access: attach()
     }
     HC(hipStreamSynchronize(st));
     barrier();  // nobody overwrites a send buffer a peer is still reading
@@ -850,6 +878,7 @@ int kgs_ctx_set_group(kgs_ctx_t* ctx, kgs_group_t* g, int rank) {
   if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
   std::lock_guard<std::mutex> lk(ctx->mu);
   if (g && (rank < 0 || rank >= g->world)) throw KgsError(KGS_E_ARG, "bad rank for this group");
+  if (g) g->attach(rank, ctx->device);
   ctx->group = g;  // a world-1 group runs the distributed code path on one rank (transport check)
   ctx->group_rank = ctx->group ? rank : 0;
   API_END

@@ -113,9 +113,15 @@ async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT) {
         // the SRS load is an async job (a libuv thread round trip) even when libkgs finds its tables
         // already resident; skip it when this context loaded the same file (same real path, size and
         // mtime — the identity libkgs checks, so a rewritten ptau is still re-read) for >= nBits
-        const st = fs.statSync(key, { bigint: true });
-        const id = `${fs.realpathSync(key)}#${st.size}#${st.mtimeNs}`;
-        if (slot.srsId !== id || slot.srsBits < nBits) {
+        // (a file that cannot be stat'ed goes to libkgs, which reports it as the drop-in always has)
+        let id = null;
+        try {
+            const st = fs.statSync(key, { bigint: true });
+            id = `${fs.realpathSync(key)}#${st.size}#${st.mtimeNs}`;
+        } catch (e) {
+            id = null;
+        }
+        if (id === null || slot.srsId !== id || slot.srsBits < nBits) {
             slot.srsId = null;
             await load().srsLoadPtau(slot.ctx, key, nBits);
             slot.srsId = id;
