@@ -41,6 +41,7 @@ struct MsmTables {
   int c = 0, W = 0;
 };
 
+constexpr int MSM_SL_G_MAX = 128;  // chunks per partition the lo-pass count buffer holds (msm.hip SL_G)
 struct MsmWork {
   int32_t* digit = nullptr;  // reused as the partition-pass value array
   uint8_t* lo = nullptr;
@@ -48,10 +49,15 @@ struct MsmWork {
   uint32_t *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *sorted = nullptr;
   uint32_t* part = nullptr;      // bucket row + column sums (2^h + 2^l run records, msm.hip k_rowcol)
   uint32_t* segowner = nullptr;  // bucket of each segment's first run
-  uint32_t* locnt = nullptr;     // lo pass: 256 partitions x 256 lo x 64 chunks counts / bases
+  uint32_t* locnt = nullptr;     // lo pass: 256 partitions x 256 lo x MSM_SL_G_MAX chunks counts / bases
   uint32_t* chunklist = nullptr; // combine levels: 3 lists of chunk-start segments
   uint32_t* chunkcnt = nullptr;  // their lengths
   uint32_t* raw29 = nullptr;     // accumulate output in the fq29 form (B + 1 + nseg entries x 160 B)
+  // paired accumulation (msm.hip k_pair_*): prefix product per pair slot (9 limb planes per slot,
+  // segment-major within a plane), per-segment totals and their inverses (packed fq)
+  uint32_t* pair_pref = nullptr;
+  uint64_t pair_words = 0;
+  uint32_t *pair_tot = nullptr, *pair_inv = nullptr, *pair_cnt = nullptr;
 };
 
 // ntt.hip

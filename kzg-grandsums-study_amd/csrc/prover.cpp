@@ -201,11 +201,18 @@ void ensure_msm_work(kgs_ctx& c) {
     w.offsets = c.buf("msm_offsets" + sfx, 4 * (B + 4));
     w.cursor = c.buf("msm_cursor" + sfx, 4 * (B + 600));
     w.segowner = c.buf("msm_segowner" + sfx, 4 * nseg);
-    w.locnt = c.buf("msm_locnt" + sfx, 4 * 256 * 256 * 64);  // partitions x lo x chunks (msm.hip SL_G)
+    w.locnt = c.buf("msm_locnt" + sfx, 4 * 256 * 256 * (size_t)MSM_SL_G_MAX);  // partitions x lo x chunks
     w.chunklist = c.buf("msm_chunklist" + sfx, 4 * 3 * (nseg / 16 + B + 16));
     w.chunkcnt = c.buf("msm_chunkcnt" + sfx, 64);
     w.raw29 = c.buf("msm_raw29" + sfx, 160 * ((size_t)B + 2 + nseg));
     w.part = c.buf("msm_part" + sfx, 160 * (size_t)(2 << (cc / 2)));  // row + column sums
+    if (getenv("KGS_ACC_PAIRS")) {  // paired accumulation (A/B): ceil(L/2) slots x 9 limbs per segment
+      w.pair_words = (E / 2 + 2 * nseg) * 9;
+      w.pair_pref = c.buf("msm_pair_pref" + sfx, 4 * w.pair_words);
+      w.pair_tot = c.buf("msm_pair_tot" + sfx, 32 * nseg);
+      w.pair_inv = c.buf("msm_pair_inv" + sfx, 32 * nseg);
+      w.pair_cnt = c.buf("msm_pair_cnt" + sfx, 4 * nseg);
+    }
   }
   c.work_npts = npts;
 }
