@@ -47,8 +47,6 @@ constexpr L9 C256 = {{0x058f0d9du, 0x1aea1c6eu, 0x11c2cf74u, 0x11d651ebu, 0x1462
                       0x183340fbu, 0x000e0a77u}};  // 2^256 mod q: mul(x*2^261, C256) = x*2^256
 constexpr L9 C266 = {{0x13349ca1u, 0x1a5d84a8u, 0x0a3e5cacu, 0x100249e0u, 0x12b951e8u, 0x0e92d304u, 0x14cb95b3u,
                       0x041b9d3du, 0x00058003u}};  // 2^266 mod q: mul(x*2^256, C266) = x*2^261
-constexpr L9 C271 = {{0x1d1c9c4bu, 0x08a372eeu, 0x1273abadu, 0x17c9d397u, 0x1698b0a7u, 0x09c89e50u, 0x177e12abu,
-                      0x185f3518u, 0x001ed378u}};  // 2^271 mod q: fq::inverse_bgcd of x*2^261 is x^-1*2^251
 // 2^261 mod q as 8 x 32-bit words: fq (R = 2^256) product t * C261W turns x*2^256 into x*2^261
 constexpr uint32_t C261W[8] = {0x157ccc21u, 0x4e8384ebu, 0x0ce148c3u, 0xfb90a602u,
                                0x819caa36u, 0x5301fa84u, 0x563d4475u, 0x0dc83629u};
@@ -312,15 +310,10 @@ struct g1_acc29 {
 #pragma unroll
     for (int i = 0; i < 8; i++) z |= xw[i] | yw[i];
     if (z == 0) return;  // affine infinity
-    add_aff_limbs(fq29::unpack(xw), fq29::unpack(yw), negy);
-  }
-
-  // this += (x2, +-y2) for coordinates already in limbs (normalised; x2 < 3.1q, y2 < 2.1q: the pair
-  // sums of k_pair_bwd, bounds in tests/test_field29.py) — add_aff after its infinity test and unpack
-  __device__ __forceinline__ void add_aff_limbs(const fq29& x2, const fq29& y2, bool negy) {
+    const fq29 x2 = fq29::unpack(xw), y2 = fq29::unpack(yw);
     if (inf) {
       X = x2;
-      const fq29 yn = fq29::neg<4, 1>(y2).norm();
+      const fq29 yn = fq29::neg<2, 1>(y2).norm();
 #pragma unroll
       for (int j = 0; j < 9; j++) Y.l[j] = negy ? yn.l[j] : y2.l[j];
       ZZ = fq29::from(f29::ONE);

@@ -53,11 +53,6 @@ struct MsmWork {
   uint32_t* chunklist = nullptr; // combine levels: 3 lists of chunk-start segments
   uint32_t* chunkcnt = nullptr;  // their lengths
   uint32_t* raw29 = nullptr;     // accumulate output in the fq29 form (B + 1 + nseg entries x 160 B)
-  // paired accumulation (msm.hip k_pair_*): prefix product per pair slot (9 limb planes per slot,
-  // segment-major within a plane), per-segment totals and their inverses (packed fq)
-  uint32_t* pair_pref = nullptr;
-  uint64_t pair_words = 0;
-  uint32_t *pair_tot = nullptr, *pair_inv = nullptr, *pair_cnt = nullptr;
 };
 
 // ntt.hip

@@ -685,286 +685,6 @@ extern "C" int kgs_diag_clock(double* ghz, int* nblocks) {
 }
 #endif
 
-// ------------------------------------------------------------------ paired bucket accumulation
-// (KGS_ACC_PAIRS=1; A/B against k_accumulate.) The XYZZ mixed add costs 9 Montgomery reductions per
-// bucket entry. Two entries of one bucket can first be added AFFINE — lambda = (y2 - y1) / (x2 - x1),
-// x3 = lambda^2 - x1 - x2, y3 = lambda (x1 - x3) - y1: 4 reductions once the inversion is shared —
-// and their sum then enters the bucket with ONE mixed add: 13 reductions per two entries instead of
-// 18. The inversions of all pairs of the MSM are shared (Montgomery's trick over the whole MSM):
-//   k_pair_fwd  per segment (the same fixed-size segments as k_accumulate): the runs of each bucket
-//               inside it, entries paired (r0, r0+1), (r0+2, r0+3), ...; d = x2 - x1 of each pair and
-//               the running prefix product, stored per pair slot (x coordinates gathered only);
-//   k_pair_inv  the inverse of every segment's total (per-block prefix / suffix products, one binary-
-//               Euclid inversion per block);
-//   k_pair_bwd  per segment, runs and pairs in reverse: 1/d of each pair from the stored prefix and the
-//               running inverse, the affine sum, then one mixed add into the run's accumulator; run
-//               records, segment owners and combine lists exactly as k_accumulate writes them.
-// A pair is not formed (both entries are added singly) when an x coordinate is 0 (table infinity
-// (0, 0), or a point with x = 0) or x1 == x2 mod q (equal or opposite points): both kernels decide it
-// from the same values, so they agree on every slot.
-constexpr uint32_t PAIR_LIMBS = 9;
-__device__ __forceinline__ bool pair_x_zero(const uint4& a, const uint4& b) {
-  return ((a.x | a.y | a.z | a.w) | (b.x | b.y | b.z | b.w)) == 0;
-}
-// x2 - x1 (table x coordinates, canonical < q) -> normalised, in (0, 2q); *skip when it is 0 mod q
-__device__ __forceinline__ fq29 pair_d(const fq29& x1, const fq29& x2, bool& zero) {
-  const fq29 d = fq29::sub<1, 1>(x2, x1).norm();
-  zero = d.maybe_zero8() && d.to_fq().is_zero();
-  return d;
-}
-__device__ __forceinline__ const uint4* pair_pt(const uint32_t* table, uint32_t v) {
-  return reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(v & 0x7fffffffu));
-}
-// first bucket b with offsets[b + 1] > e, searching up from b
-__device__ __forceinline__ uint32_t bucket_from(const uint32_t* offsets, uint32_t b, uint32_t e) {
-  while (offsets[b + 1] <= e) b++;
-  return b;
-}
-__device__ __forceinline__ uint32_t bucket_of(const uint32_t* offsets, uint32_t nbins, uint32_t e) {
-  uint32_t lo = 0, hi = nbins;  // offsets[lo] <= e < offsets[hi]
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (offsets[mid] <= e) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-
-__global__ void __launch_bounds__(256) k_pair_fwd(const uint32_t* __restrict__ sorted,
-                                                  const uint32_t* __restrict__ offsets, uint32_t nbins,
-                                                  const uint32_t* __restrict__ table, uint32_t L, uint32_t T,
-                                                  uint32_t* __restrict__ pref, uint32_t* __restrict__ tot,
-                                                  uint32_t* __restrict__ npairs) {
-  KGS_AUX_PRIO();
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= T) return;
-  const uint32_t E = offsets[nbins];
-  const uint32_t start = s * L;
-  fq29 acc = fq29::from(f29::ONE);
-  uint32_t k = 0;
-  if (start < E) {
-    // one flat loop (every lane steps through its segment at the same pace): a step takes the pair
-    // (e, e + 1) when both lie in the current run, else the run's odd last entry alone
-    const uint32_t end = start + L < E ? start + L : E;
-    uint32_t b = bucket_of(offsets, nbins, start);
-    uint32_t r1 = offsets[b + 1] < end ? offsets[b + 1] : end;
-    // software pipeline: the indices and x coordinates of the next step's pair candidate (e, e + 1)
-    // are loaded while the current pair's product runs (clamped to the segment: always valid)
-    const uint32_t last = end - 1;
-    uint32_t v1 = sorted[start], v2 = sorted[start + 1 <= last ? start + 1 : last];
-    uint4 a0 = pair_pt(table, v1)[0], a1 = pair_pt(table, v1)[1], c0 = pair_pt(table, v2)[0], c1 = pair_pt(table, v2)[1];
-    for (uint32_t e = start; e < end;) {
-      if (e >= r1) {
-        b = bucket_from(offsets, b + 1, e);
-        r1 = offsets[b + 1] < end ? offsets[b + 1] : end;
-      }
-      const bool pair = e + 1 < r1;
-      const uint32_t en = e + (pair ? 2 : 1);  // the next step's first entry
-      const uint32_t w1 = sorted[en <= last ? en : last], w2 = sorted[en + 1 <= last ? en + 1 : last];
-      const uint4* q1 = pair_pt(table, w1);
-      const uint4* q2 = pair_pt(table, w2);
-      const uint4 n0 = q1[0], n1 = q1[1], m0 = q2[0], m1 = q2[1];
-      if (pair && !pair_x_zero(a0, a1) && !pair_x_zero(c0, c1)) {
-        const uint32_t xw1[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-        const uint32_t xw2[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-        bool zero;
-        const fq29 d = pair_d(fq29::unpack(xw1), fq29::unpack(xw2), zero);
-        if (!zero) {
-          acc = k ? fq29::mul(acc, d) : d;
-          uint32_t* o = pref + (uint64_t)k * PAIR_LIMBS * T + s;
-#pragma unroll
-          for (uint32_t j = 0; j < PAIR_LIMBS; j++) o[(uint64_t)j * T] = acc.l[j];
-          k++;
-        }
-      }
-      // (the odd last entry of a run is added singly by k_pair_bwd)
-      e = en;
-      a0 = n0; a1 = n1; c0 = m0; c1 = m1;
-    }
-  }
-  npairs[s] = k;
-  // the segment's total (1 without pairs), canonical 256-bit words for k_pair_inv
-  fq t;
-  acc.pack(t.v);
-  fq::reduce_once(fq::reduce_once(t)).store(tot + 8 * (uint64_t)s);
-}
-
-// inverse of every segment total t (values x*2^261): fq's Montgomery inverse of t is 2^512/t, times
-// 2^10 (one product by 2^266 mod q) = x^-1 * 2^261. 256 threads x 4 totals per block (4 waves: the
-// block fits beside two resident accumulate waves per SIMD), one inversion per block.
-constexpr int PINV_T = 256, PINV_V = 4;
-__global__ void __launch_bounds__(PINV_T) k_pair_inv(uint32_t* __restrict__ inv, const uint32_t* __restrict__ tot,
-                                                     uint32_t T) {
-  KGS_AUX_PRIO();
-  __shared__ uint32_t lds[PINV_T * 8];
-  __shared__ uint32_t tinv[8];
-  const uint32_t t = threadIdx.x, i0 = (blockIdx.x * PINV_T + t) * PINV_V;
-  const fq one = fq::one();
-  fq v[PINV_V], run = one;
-#pragma unroll
-  for (int j = 0; j < PINV_V; j++) {
-    v[j] = i0 + j < T ? fq::load(tot + 8 * (uint64_t)(i0 + j)) : one;
-    run = run * v[j];
-  }
-  fq pre = run;  // inclusive prefix over the block's threads
-  for (uint32_t off = 1; off < PINV_T; off <<= 1) {
-    pre.store(lds + 8 * t);
-    __syncthreads();
-    if (t >= off) pre = fq::load(lds + 8 * (t - off)) * pre;
-    __syncthreads();
-  }
-  if (t == PINV_T - 1) pre.inverse_bgcd().store(tinv);  // the block total: one lane, binary Euclid
-  pre.store(lds + 8 * t);
-  __syncthreads();
-  // inverse of this thread's product: 1/total x (prefix of the threads after it) — walk down
-  // from the total: inv(prefix_t) = inv(total) x prod_{u > t} run_u; cheaper to recover as
-  // inv(run_t) = inv(prefix_t) x prefix_{t-1}
-  const fq pex = t ? fq::load(lds + 8 * (t - 1)) : one;
-  __syncthreads();
-  // suffix products of the runs (exclusive): for inv(prefix_t)
-  fq suf = run;
-  for (uint32_t off = 1; off < PINV_T; off <<= 1) {
-    suf.store(lds + 8 * t);
-    __syncthreads();
-    if (t + off < PINV_T) suf = suf * fq::load(lds + 8 * (t + off));
-    __syncthreads();
-  }
-  suf.store(lds + 8 * t);
-  __syncthreads();
-  const fq sex = t + 1 < PINV_T ? fq::load(lds + 8 * (t + 1)) : one;
-  fq c266;
-  {
-    const fq29 c = fq29::from(f29::C266);
-    c.pack(c266.v);  // 2^266 mod q < q: packs canonically
-  }
-  fq acc = fq::load(tinv) * pex * sex * c266;  // 1 / run_t (x 2^10)
-  // the thread's values: inv(v_j) = acc x (product of the others), backward
-  fq pf[PINV_V];
-  pf[0] = one;
-#pragma unroll
-  for (int j = 1; j < PINV_V; j++) pf[j] = pf[j - 1] * v[j - 1];
-#pragma unroll
-  for (int j = PINV_V - 1; j >= 0; j--) {
-    if (i0 + j < T) (acc * pf[j]).store(inv + 8 * (uint64_t)(i0 + j));
-    acc = acc * v[j];
-  }
-}
-
-template <int VW>
-__global__ void __launch_bounds__(256, VW) k_pair_bwd(uint32_t* __restrict__ segowner,
-                                                  uint32_t* __restrict__ chunklist, uint32_t* __restrict__ chunkcnt,
-                                                  const uint32_t* __restrict__ sorted,
-                                                  const uint32_t* __restrict__ offsets, uint32_t nbins,
-                                                  const uint32_t* __restrict__ table, uint32_t L, uint32_t T,
-                                                  const uint32_t* __restrict__ pref, const uint32_t* __restrict__ inv,
-                                                  const uint32_t* __restrict__ npairs, uint32_t* __restrict__ raw) {
-  if (VW == 2) asm volatile("; reserve v175 (176 VGPRs: two waves per SIMD)" ::: "v175");
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= T) return;
-  const uint32_t E = offsets[nbins];
-  const uint32_t start = s * L;
-  if (start >= E) return;
-  const uint32_t end = start + L < E ? start + L : E;
-  const uint32_t b0 = bucket_of(offsets, nbins, start);
-  const uint32_t o0 = offsets[b0];
-  segowner[s] = b0;
-  combine_enqueue(chunklist, chunkcnt, s, o0, offsets[b0 + 1], L, 1);
-  uint32_t k = npairs[s];  // slots k_pair_fwd filled; the reverse walk reads slot k - 1 before the k-th pair
-  const fq29 one29 = fq29::from(f29::ONE);
-  fq29 I = fq29::unpack(inv + 8 * (uint64_t)s);  // 1 / (product of all pairs' d), x*2^261 form
-  // one flat loop from the segment's end down (every lane at the same pace, one mixed add per
-  // step): the run's odd last entry alone, then its pairs (r0 + 2i, r0 + 2i + 1) from the top; a pair
-  // that is not formed adds its first entry now and its second at the next step; at a run's start its
-  // accumulator leaves as the run's record (as in k_accumulate)
-  uint32_t b = bucket_of(offsets, nbins, end - 1);
-  uint32_t r0 = offsets[b] > start ? offsets[b] : start;
-  g1_acc29 acc;
-  acc.set_inf();
-  uint32_t e = end, pend = 0xffffffffu;
-  while (e > start || pend != 0xffffffffu) {
-    if (pend == 0xffffffffu && e <= r0) {  // run [r0, ...) done
-      acc.store_raw(run_rec(raw, r0 == start && start != o0 ? nbins + s : b));
-      acc.set_inf();
-      b--;
-      while (offsets[b] >= e) b--;  // empty buckets
-      r0 = offsets[b] > start ? offsets[b] : start;
-    }
-    fq29 px, py;
-    bool negy = false, inf = false;
-    auto single = [&](uint32_t v) {
-      const uint4* p = pair_pt(table, v);
-      const uint4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
-      const uint32_t xw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      const uint32_t yw[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
-      uint32_t z = 0;
-#pragma unroll
-      for (int i = 0; i < 8; i++) z |= xw[i] | yw[i];
-      inf = z == 0;  // affine infinity: nothing to add (g1_acc29::add_aff)
-      px = fq29::unpack(xw);
-      py = fq29::unpack(yw);
-      negy = (v & 0x80000000u) != 0;
-    };
-    if (pend != 0xffffffffu) {
-      single(pend);
-      pend = 0xffffffffu;
-    } else if ((e - r0) & 1u) {
-      single(sorted[--e]);
-    } else {
-      e -= 2;
-      const uint32_t v1 = sorted[e], v2 = sorted[e + 1];
-      const uint4* p1 = pair_pt(table, v1);
-      const uint4* p2 = pair_pt(table, v2);
-      const uint4 a0 = p1[0], a1 = p1[1], c0 = p2[0], c1 = p2[1];
-      bool zero = pair_x_zero(a0, a1) || pair_x_zero(c0, c1);
-      const uint32_t xw1[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      const uint32_t xw2[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-      const fq29 x1 = fq29::unpack(xw1), x2 = fq29::unpack(xw2);
-      fq29 d = x1;
-      if (!zero) d = pair_d(x1, x2, zero);
-      if (zero) {
-        single(v1);
-        pend = v2;
-      } else {
-        k--;
-        fq29 pre = one29;
-        if (k) {
-          const uint32_t* o = pref + (uint64_t)(k - 1) * PAIR_LIMBS * T + s;
-#pragma unroll
-          for (uint32_t j = 0; j < PAIR_LIMBS; j++) pre.l[j] = o[(uint64_t)j * T];
-        }
-        const fq29 invd = fq29::mul(I, pre);  // 1 / d
-        I = fq29::mul(I, d);
-        const uint4 a2 = p1[2], a3 = p1[3], c2 = p2[2], c3 = p2[3];
-        const uint32_t yw1[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
-        const uint32_t yw2[8] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-        // y with the entries' signs: q - y for a negated point (y canonical < q)
-        fq29 y1 = fq29::unpack(yw1), y2 = fq29::unpack(yw2);
-        if (v1 & 0x80000000u) y1 = fq29::neg<1, 1>(y1).norm();
-        if (v2 & 0x80000000u) y2 = fq29::neg<1, 1>(y2).norm();
-        const fq29 lam = fq29::mul(fq29::sub<2, 1>(y2, y1).norm(), invd);                     // < 1.1q
-        px = fq29::sub<2, 2>(fq29::sqr(lam), fq29::add(x1, x2)).norm();                          // < 3.1q
-        py = fq29::sub<1, 1>(fq29::mul(lam, fq29::sub<4, 1>(x1, px).norm()), y1).norm();         // < 2.1q
-      }
-    }
-    if (!inf) acc.add_aff_limbs(px, py, negy);
-  }
-  acc.store_raw(run_rec(raw, r0 == start && start != o0 ? nbins + s : b));
-}
-
-void msm_pairs_run(hipStream_t st, const MsmTables& tb, MsmWork& w, uint32_t nbins, uint32_t L, uint64_t nseg,
-                   uint32_t* cnt, bool exclusive_acc) {
-  const uint32_t T = (uint32_t)nseg;
-  hipLaunchKernelGGL(k_pair_fwd, dim3(nb(nseg)), dim3(256), 0, st, w.sorted, w.offsets, nbins, tb.table, L, T,
-                     w.pair_pref, w.pair_tot, w.pair_cnt);
-  hipLaunchKernelGGL(k_pair_inv, dim3((unsigned)((nseg + PINV_T * PINV_V - 1) / (PINV_T * PINV_V))), dim3(PINV_T), 0, st,
-                     w.pair_inv, w.pair_tot, T);
-  if (exclusive_acc)
-    hipLaunchKernelGGL(k_pair_bwd<2>, dim3(nb(nseg)), dim3(256), 0, st, w.segowner, w.chunklist, cnt, w.sorted,
-                       w.offsets, nbins, tb.table, L, T, w.pair_pref, w.pair_inv, w.pair_cnt, w.raw29);
-  else
-    hipLaunchKernelGGL(k_pair_bwd<3>, dim3(nb(nseg)), dim3(256), 0, st, w.segowner, w.chunklist, cnt, w.sorted,
-                       w.offsets, nbins, tb.table, L, T, w.pair_pref, w.pair_inv, w.pair_cnt, w.raw29);
-}
-
 // Bucket totals. Bucket b = its start record (run_rec b) + the partials of the segments whose start
 // lies strictly inside it: segments s_lo(b) = offsets[b]/L + 1 .. s_hi(b) = ceil(offsets[b+1]/L) - 1.
 // Buckets can be arbitrarily skewed (a selector polynomial has all-equal coefficients, so every point
@@ -1157,13 +877,7 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   uint32_t* cnt = w.chunkcnt;
   const uint64_t lcap = nseg / CB_T + B + 16;
   hipMemsetAsync(cnt, 0, 4 * CB_LEVELS, st);
-  static const bool pairs = [] {
-    const char* e = getenv("KGS_ACC_PAIRS");
-    return e && e[0] == '1';
-  }();
-  if (pairs && w.pair_pref && (uint64_t)((L + 1) / 2) * PAIR_LIMBS * nseg <= w.pair_words)
-    msm_pairs_run(st, tb, w, B + 1, (uint32_t)L, nseg, cnt, exclusive_acc);
-  else if (exclusive_acc)
+  if (exclusive_acc)
     hipLaunchKernelGGL(k_accumulate<2>, dim3(nb(nseg)), dim3(256), 0, st, w.segowner, w.chunklist, cnt, w.sorted,
                        w.offsets, B + 1, tb.table, (uint32_t)L, w.raw29);
   else

@@ -206,13 +206,6 @@ void ensure_msm_work(kgs_ctx& c) {
     w.chunkcnt = c.buf("msm_chunkcnt" + sfx, 64);
     w.raw29 = c.buf("msm_raw29" + sfx, 160 * ((size_t)B + 2 + nseg));
     w.part = c.buf("msm_part" + sfx, 160 * (size_t)(2 << (cc / 2)));  // row + column sums
-    if (getenv("KGS_ACC_PAIRS")) {  // paired accumulation (A/B): ceil(L/2) slots x 9 limbs per segment
-      w.pair_words = (E / 2 + 2 * nseg) * 9;
-      w.pair_pref = c.buf("msm_pair_pref" + sfx, 4 * w.pair_words);
-      w.pair_tot = c.buf("msm_pair_tot" + sfx, 32 * nseg);
-      w.pair_inv = c.buf("msm_pair_inv" + sfx, 32 * nseg);
-      w.pair_cnt = c.buf("msm_pair_cnt" + sfx, 4 * nseg);
-    }
   }
   c.work_npts = npts;
 }
