@@ -31,7 +31,7 @@ const { getCurveFromName, Evaluations, mset_eq_kzg_grandsum_prover, mset_eq_kzg_
             }
             return o;
         } catch (e) {
-            return { error: e.message };
+            return { error: e.message, errorName: e.name };
         }
     };
     let out;

@@ -451,3 +451,39 @@ def test_js_rewritten_ptau_is_reread(tmp_path):
     got = [p["commitments"] for p in out["proofs"]]
     assert got[0] == expect[0] and got[1] == expect[0]
     assert got[2] == expect[1] and got[3] == expect[1]
+
+
+@pytest.mark.gpu
+def test_js_reference_quirks(tmp_path):
+    """Degenerate valid multisets through the JS drop-in (DESIGN.md §4 "Reference quirks",
+    tests/test_gpu_quirks.py): by default the module proves them (byte-identical to the oracle's
+    exact-value semantics, verified by the drop-in verifier); with KGS_REFERENCE_QUIRKS=1 it throws what
+    the reference throws — an Error with its message, or V8's RangeError for a zero quotient."""
+    import test_gpu_quirks as Q
+    ptau = common.oracle_ptau(9)
+    srs = P.SRS(ptau, common.tau())
+    plan = [("grandsum", "x", False), ("grandproduct", "x", False), ("grandproduct", "affine", True),
+            ("grandsum", "same", False)]
+    cases, exact, ref = [], [], []
+    for kind, name, sel in plan:
+        Fs, Ts, sF, sT = Q.inputs(name, 4, 1, sel)
+        cases.append({"kind": kind, "F": [Fs[0].hex()], "T": [Ts[0].hex()],
+                      "selF": sF.hex() if sF else None, "selT": sT.hex() if sT else None})
+        ex = Q.oracle_outcome(kind, ptau, Fs, Ts, sF, sT, quirks=False)
+        exact.append({sec: {k: v.hex() for k, v in ex[1][sec].items()} for sec in ("commitments", "evaluations")})
+        ref.append(Q.oracle_outcome(kind, ptau, Fs, Ts, sF, sT, quirks=True))
+    spec = tmp_path / "spec.json"
+    spec.write_text(json.dumps({"ptau": ptau, "cases": cases, "verify": True}))
+    for quirks in (False, True):
+        env = {k: v for k, v in os.environ.items() if k != "KGS_REFERENCE_QUIRKS"}
+        if quirks:
+            env["KGS_REFERENCE_QUIRKS"] = "1"
+        out = json.loads(subprocess.check_output([NODE, os.path.join(JS, "test", "prove_from_json.js"), str(spec)],
+                                                 timeout=600, env=env))
+        for got, ex, rf in zip(out["proofs"], exact, ref):
+            if not quirks:
+                assert {"commitments": got["commitments"], "evaluations": got["evaluations"]} == ex
+                assert got["verified"] is True
+            else:
+                assert rf[0] in ("Error", "RangeError")
+                assert got["error"] == rf[1] and got["errorName"] == rf[0]
