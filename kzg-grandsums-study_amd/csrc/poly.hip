@@ -16,6 +16,14 @@ namespace kgs {
 
 static inline unsigned nb(uint64_t work, unsigned bs = 256) { return (unsigned)((work + bs - 1) / bs); }
 
+// Threads of the single-block tile scans (k_tile_inverse, k_tile_carry, k_div_carries). A/B knob: a
+// 1024-thread block needs four free wave slots of its VGPR size on every SIMD of one CU at once,
+// which two resident accumulate waves per SIMD (other proofs in flight) do not leave.
+#ifndef KGS_SCAN_NT
+#define KGS_SCAN_NT 1024
+#endif
+constexpr uint32_t SCAN_NT = KGS_SCAN_NT;
+
 __device__ __forceinline__ uint32_t brev(uint32_t x, int bits) {
   return bits ? __builtin_bitreverse32(x) >> (32 - bits) : 0;
 }
@@ -151,32 +159,32 @@ __global__ void __launch_bounds__(256) k_builder_tileprod(uint32_t* __restrict__
 }
 
 // Single block: inverse of every tile product via prefix/suffix products and ONE inversion.
-__global__ void __launch_bounds__(1024) k_tile_inverse(uint32_t* __restrict__ tinv, const uint32_t* __restrict__ tp,
+__global__ void __launch_bounds__(SCAN_NT) k_tile_inverse(uint32_t* __restrict__ tinv, const uint32_t* __restrict__ tp,
                                                        uint32_t ntiles) {
   KGS_AUX_PRIO();
-  __shared__ uint32_t lds[1024 * 8];
+  __shared__ uint32_t lds[SCAN_NT * 8];
   __shared__ uint32_t tot[8];
   const uint32_t t = threadIdx.x;
-  const uint32_t per = (ntiles + 1023) / 1024;
+  const uint32_t per = (ntiles + SCAN_NT - 1) / SCAN_NT;
   const uint32_t lo = t * per, hi = lo + per < ntiles ? lo + per : ntiles;
   fr p = fr::one();
   for (uint32_t b = lo; b < hi; b++) p = p * fr::load(tp + 8 * b);
   // inclusive prefix over threads
   fr pre = p;
-  for (uint32_t off = 1; off < 1024; off <<= 1) {
+  for (uint32_t off = 1; off < SCAN_NT; off <<= 1) {
     pre.store(lds + 8 * t);
     __syncthreads();
     if (t >= off) pre = fr::load(lds + 8 * (t - off)) * pre;
     __syncthreads();
   }
   fr suf = p;
-  for (uint32_t off = 1; off < 1024; off <<= 1) {
+  for (uint32_t off = 1; off < SCAN_NT; off <<= 1) {
     suf.store(lds + 8 * t);
     __syncthreads();
-    if (t + off < 1024) suf = suf * fr::load(lds + 8 * (t + off));
+    if (t + off < SCAN_NT) suf = suf * fr::load(lds + 8 * (t + off));
     __syncthreads();
   }
-  if (t == 1023) {
+  if (t == SCAN_NT - 1) {
     fr total_inv = pre.inverse_bgcd();  // one lane: binary Euclid (~5x fewer instructions than Fermat)
     total_inv.store(tot);
   }
@@ -189,7 +197,7 @@ __global__ void __launch_bounds__(1024) k_tile_inverse(uint32_t* __restrict__ ti
   __syncthreads();
   suf.store(lds + 8 * t);
   __syncthreads();
-  fr sex = t < 1023 ? fr::load(lds + 8 * (t + 1)) : fr::one();
+  fr sex = t < SCAN_NT - 1 ? fr::load(lds + 8 * (t + 1)) : fr::one();
   // inverse of this thread's group product, then walk its tiles
   fr ginv = total_inv * pex * sex;
   // within group: inverse of tile b = ginv * (prod of other tiles in group)
@@ -293,16 +301,16 @@ __global__ void __launch_bounds__(256) k_builder_finish(uint32_t* __restrict__ o
 
 // Single block: exclusive scan of tile accumulators -> carry per tile (in place).
 template <bool PROD>
-__global__ void __launch_bounds__(1024) k_tile_carry(uint32_t* __restrict__ acc, uint32_t ntiles) {
+__global__ void __launch_bounds__(SCAN_NT) k_tile_carry(uint32_t* __restrict__ acc, uint32_t ntiles) {
   KGS_AUX_PRIO();
-  __shared__ uint32_t lds[1024 * 8];
+  __shared__ uint32_t lds[SCAN_NT * 8];
   const uint32_t t = threadIdx.x;
-  const uint32_t per = (ntiles + 1023) / 1024;
+  const uint32_t per = (ntiles + SCAN_NT - 1) / SCAN_NT;
   const uint32_t lo = t * per, hi = lo + per < ntiles ? lo + per : ntiles;
   fr s = PROD ? fr::one() : fr::zero();
   for (uint32_t b = lo; b < hi; b++) s = PROD ? s * fr::load(acc + 8 * b) : s + fr::load(acc + 8 * b);
   fr inc = s;
-  for (uint32_t off = 1; off < 1024; off <<= 1) {
+  for (uint32_t off = 1; off < SCAN_NT; off <<= 1) {
     inc.store(lds + 8 * t);
     __syncthreads();
     if (t >= off) inc = PROD ? fr::load(lds + 8 * (t - off)) * inc : fr::load(lds + 8 * (t - off)) + inc;
@@ -345,10 +353,10 @@ void launch_builder(hipStream_t st, bool prod, bool sel, uint32_t* out, const ui
   const uint32_t ntiles = (uint32_t)((n + BT_TILE - 1) / BT_TILE);
 #define KGS_BUILD(P, S)                                                                                      \
   hipLaunchKernelGGL((k_builder_tileprod<P, S>), dim3(ntiles), dim3(256), 0, st, scratch_tp, f, t, sf, stt, gamma, n); \
-  hipLaunchKernelGGL(k_tile_inverse, dim3(1), dim3(1024), 0, st, scratch_ti, scratch_tp, ntiles);                   \
+  hipLaunchKernelGGL(k_tile_inverse, dim3(1), dim3(SCAN_NT), 0, st, scratch_ti, scratch_tp, ntiles);                   \
   hipLaunchKernelGGL((k_builder_finish<P, S>), dim3(ntiles), dim3(256), 0, st, out, scratch_tp, scratch_ti, f, t, sf, \
                      stt, gamma, n);                                                                                  \
-  hipLaunchKernelGGL((k_tile_carry<P>), dim3(1), dim3(1024), 0, st, scratch_tp, ntiles);                             \
+  hipLaunchKernelGGL((k_tile_carry<P>), dim3(1), dim3(SCAN_NT), 0, st, scratch_tp, ntiles);                             \
   hipLaunchKernelGGL((k_apply_carry<P>), dim3(nb(n)), dim3(256), 0, st, out, scratch_tp, n, flag);
   if (prod) {
     if (sel) { KGS_BUILD(true, true) } else { KGS_BUILD(true, false) }
@@ -470,12 +478,12 @@ void launch_eval_tiles(hipStream_t st, uint32_t* part, const EvalBatch& eb, cons
 // ---------------------------------------------------------------------------- synthetic division
 // r_i = a_i + z r_{i+1} (r_L = 0); quotient q_{i-1} = r_i; r_0 must be 0.
 // tile carries: carry[b] = r_{start of tile b+1}, from tile Horner values h_b (part) with Z = z^2048.
-__global__ void __launch_bounds__(1024) k_div_carries(uint32_t* __restrict__ carry, const uint32_t* __restrict__ h,
+__global__ void __launch_bounds__(SCAN_NT) k_div_carries(uint32_t* __restrict__ carry, const uint32_t* __restrict__ h,
                                                       uint32_t ntiles, const uint32_t* __restrict__ zT) {
   KGS_AUX_PRIO();
-  __shared__ uint32_t lds[1024 * 8];
+  __shared__ uint32_t lds[SCAN_NT * 8];
   const uint32_t t = threadIdx.x;
-  const uint32_t per = (ntiles + 1023) / 1024;
+  const uint32_t per = (ntiles + SCAN_NT - 1) / SCAN_NT;
   const uint32_t lo = t * per, hi = lo + per < ntiles ? lo + per : ntiles;
   const fr Z = fr::load(zT);
   // group value: sum_{b in [lo,hi)} h_b Z^(b-lo), and Z^(hi-lo)
@@ -484,14 +492,14 @@ __global__ void __launch_bounds__(1024) k_div_carries(uint32_t* __restrict__ car
   for (uint32_t b = lo; b < hi; b++) zp = zp * Z;
   // suffix scan over groups: V_t = v_t + zp_t * V_{t+1}; multipliers compose by product
   fr V = v, M = zp;
-  for (uint32_t off = 1; off < 1024; off <<= 1) {
+  for (uint32_t off = 1; off < SCAN_NT; off <<= 1) {
     V.store(lds + 8 * t);
     __syncthreads();
-    fr Vn = t + off < 1024 ? fr::load(lds + 8 * (t + off)) : fr::zero();
+    fr Vn = t + off < SCAN_NT ? fr::load(lds + 8 * (t + off)) : fr::zero();
     __syncthreads();
     M.store(lds + 8 * t);
     __syncthreads();
-    fr Mn = t + off < 1024 ? fr::load(lds + 8 * (t + off)) : fr::one();
+    fr Mn = t + off < SCAN_NT ? fr::load(lds + 8 * (t + off)) : fr::one();
     __syncthreads();
     V = V + M * Vn;
     M = M * Mn;
@@ -499,7 +507,7 @@ __global__ void __launch_bounds__(1024) k_div_carries(uint32_t* __restrict__ car
   // V is now the inclusive suffix value at group start lo; carry-in for this group = V_{t+1}
   V.store(lds + 8 * t);
   __syncthreads();
-  fr cin = t + 1 < 1024 ? fr::load(lds + 8 * (t + 1)) : fr::zero();
+  fr cin = t + 1 < SCAN_NT ? fr::load(lds + 8 * (t + 1)) : fr::zero();
   for (uint32_t b = hi; b-- > lo;) {
     cin.store(carry + 8 * b);                 // r at start of tile b+1
     cin = fr::load(h + 8 * b) + Z * cin;      // r at start of tile b
@@ -555,7 +563,7 @@ void launch_divide(hipStream_t st, uint32_t* q, uint32_t* flag, const uint32_t* 
   eb.len[0] = L;
   hipMemsetAsync(q + 8 * (L - 1), 0, 32, st);
   hipLaunchKernelGGL(k_eval_tiles, dim3(ntiles, 1), dim3(256), 0, st, part, eb, xp, ntiles);
-  hipLaunchKernelGGL(k_div_carries, dim3(1), dim3(1024), 0, st, carry, part, ntiles, xp + 8 * 9);
+  hipLaunchKernelGGL(k_div_carries, dim3(1), dim3(SCAN_NT), 0, st, carry, part, ntiles, xp + 8 * 9);
   hipLaunchKernelGGL(k_div_finish, dim3(ntiles), dim3(256), 0, st, q, flag, a, L, carry, xp);
 }
 

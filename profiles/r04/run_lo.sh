@@ -1,22 +1,26 @@
 #!/bin/bash
-# Round 4, VERDICT r3 Next #4: k_lo_scatter's 1024-thread / 70 KB-LDS blocks vs smaller blocks.
-# Parity of each variant on the MSM tests, the lo pass alone (MSM phases at 2^20 / 2^21 / 2^24 and a
-# skewed 2^20), then the headline leg interleaved x3 (profiles/ab_bench.py).
+# Round 4, VERDICT r3 Next #4: co-residency of the 1024-thread single-block / lo-pass kernels with the
+# in-flight proofs' accumulate waves (two per SIMD at 168 VGPRs leave 176 per SIMD: a 1024-thread block
+# of > 44 VGPRs per wave cannot start on a CU until an accumulate block there drains).
+# Variants: sl_* (k_lo_scatter threads / tile), scan256 (k_tile_inverse, k_tile_carry, k_div_carries at
+# 256 threads), both256 (scan256 + 256-thread lo scatter). Parity of each variant on the MSM / golden /
+# division tests, the MSM phases alone, then the headline leg interleaved x3.
 set -e
 cd "$(dirname "$0")/../.."
 R=$PWD
 OUT=$R/gpurun_out/lo
 mkdir -p $OUT
-V="kzg-grandsums-study_amd/lib/libkgs.so kzg-grandsums-study_amd/lib_ab/sl_256_8k/libkgs.so kzg-grandsums-study_amd/lib_ab/sl_512_16k/libkgs.so kzg-grandsums-study_amd/lib_ab/sl_256_16k/libkgs.so"
+V="kzg-grandsums-study_amd/lib/libkgs.so kzg-grandsums-study_amd/lib_ab/sl_256_16k/libkgs.so kzg-grandsums-study_amd/lib_ab/sl_256_8k/libkgs.so kzg-grandsums-study_amd/lib_ab/scan256/libkgs.so kzg-grandsums-study_amd/lib_ab/both256/libkgs.so"
 for L in $V; do
-  KGS_LIB=$R/$L timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -k "msm or golden" -q -x --timeout 200 --timeout-method thread > $OUT/parity_$(basename $(dirname $L)).log 2>&1 || { tail -20 $OUT/parity_$(basename $(dirname $L)).log; exit 1; }
-  echo "$L: $(tail -1 $OUT/parity_$(basename $(dirname $L)).log)"
+  n=$(basename $(dirname $L))
+  KGS_LIB=$R/$L timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -k "msm or golden or builder or eval_and_division" -q -x --timeout 200 --timeout-method thread > $OUT/parity_$n.log 2>&1 || { tail -20 $OUT/parity_$n.log; exit 1; }
+  echo "$L: $(tail -1 $OUT/parity_$n.log)"
 done
 for L in $V; do
-  for a in "20 10" "21 10" "20 10 skew"; do
+  for a in "20 10" "20 10 skew"; do
     KGS_LIB=$R/$L timeout -k 10 120 python3 profiles/msm_loop.py $a >> $OUT/msm_phases.txt 2>&1
   done
 done
 cat $OUT/msm_phases.txt
-timeout -k 10 1000 python3 profiles/ab_bench.py 3 $V > $OUT/bench_ab.txt 2>&1 || { cat $OUT/bench_ab.txt; exit 1; }
+timeout -k 10 800 python3 profiles/ab_bench.py 2 $V > $OUT/bench_ab.txt 2>&1 || { cat $OUT/bench_ab.txt; exit 1; }
 cat $OUT/bench_ab.txt
