@@ -8,6 +8,7 @@
 #include <sys/mman.h>
 #include <map>
 #include <chrono>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -105,18 +106,24 @@ constexpr size_t HUGE = (size_t)2 << 20;
 
 size_t out_round(size_t len) { return (len + HUGE - 1) / HUGE * HUGE; }
 
-uint8_t* out_alloc(size_t len) {
-  const size_t sz = out_round(len);
-  {
-    std::lock_guard<std::mutex> lk(g_out_mu);
-    auto it = g_out_free.find(sz);
-    if (it != g_out_free.end()) {
-      void* p = it->second;
-      g_out_free.erase(it);
-      g_out_cached -= sz;
-      return (uint8_t*)p;
-    }
-  }
+// KGS_JS_OUT_POOL=N: keep N spare output buffers of each size in use READY — registered
+// (kgs_host_register, so the Montgomery write-back is DMA'd straight into the buffer handed to JS:
+// no pinned staging, no host copy) and already faulted in. A background thread tops the spares up
+// after every allocation, so the registration and first-touch cost is paid beside a proof's GPU work
+// or between proofs instead of inside one; the spares count toward the 2 GiB cache.
+int out_pool_n() {
+  static const int n = getenv("KGS_JS_OUT_POOL") ? atoi(getenv("KGS_JS_OUT_POOL")) : 0;
+  return n > 0 ? n : 0;
+}
+// KGS_JS_OUT_REGISTER=1: pin every output buffer for its life so the write-back is DMA'd in place.
+// Off by default: registering a fresh 32 MiB buffer inside the call costs more than the staging copy
+// it saves whenever the caller keeps its outputs (profiles/r03/boundary_ab.txt); implied by the pool.
+bool out_registered() {
+  static const bool reg = getenv("KGS_JS_OUT_REGISTER") != nullptr || out_pool_n() > 0;
+  return reg;
+}
+
+uint8_t* out_map(size_t sz, bool prefault) {
   // over-allocate by one huge page to align the start, then trim the ends
   void* raw = mmap(nullptr, sz + HUGE, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (raw == MAP_FAILED) return nullptr;
@@ -125,12 +132,56 @@ uint8_t* out_alloc(size_t len) {
   const uintptr_t end = (uintptr_t)raw + sz + HUGE;
   if (end > a + sz) munmap((void*)(a + sz), end - (a + sz));
   madvise((void*)a, sz, MADV_HUGEPAGE);
-  // KGS_JS_OUT_REGISTER=1: pin the buffer for its life (kgs_host_register) so the Montgomery
-  // write-back is DMA'd in place. Off by default: registering a fresh 32 MiB buffer costs more than
-  // the staging copy it saves whenever the caller keeps its outputs (profiles/r03/boundary_ab.txt)
-  static const bool reg = getenv("KGS_JS_OUT_REGISTER") != nullptr;
-  if (reg) kgs_host_register((void*)a, sz);
+  if (prefault)
+    for (size_t o = 0; o < sz; o += 4096) ((volatile uint8_t*)a)[o] = 0;
+  if (out_registered() && kgs_host_register((void*)a, sz) != KGS_OK) {
+    munmap((void*)a, sz);
+    return nullptr;
+  }
   return (uint8_t*)a;
+}
+
+std::condition_variable g_refill_cv;
+std::vector<size_t> g_refill_req;  // sizes whose spares may need topping up (under g_out_mu)
+
+void refill_loop() {
+  std::unique_lock<std::mutex> lk(g_out_mu);
+  for (;;) {
+    g_refill_cv.wait(lk, [] { return !g_refill_req.empty(); });
+    const size_t sz = g_refill_req.back();
+    g_refill_req.pop_back();
+    while ((int)g_out_free.count(sz) < out_pool_n() && g_out_cached + sz <= OUT_CACHE_MAX) {
+      lk.unlock();
+      uint8_t* p = out_map(sz, true);
+      lk.lock();
+      if (!p) break;
+      g_out_free.emplace(sz, p);
+      g_out_cached += sz;
+    }
+  }
+}
+
+void request_refill(size_t sz) {  // under g_out_mu
+  static std::once_flag once;
+  std::call_once(once, [] { std::thread(refill_loop).detach(); });
+  g_refill_req.push_back(sz);
+  g_refill_cv.notify_one();
+}
+
+uint8_t* out_alloc(size_t len) {
+  const size_t sz = out_round(len);
+  {
+    std::lock_guard<std::mutex> lk(g_out_mu);
+    auto it = g_out_free.find(sz);
+    if (out_pool_n() > 0) request_refill(sz);
+    if (it != g_out_free.end()) {
+      void* p = it->second;
+      g_out_free.erase(it);
+      g_out_cached -= sz;
+      return (uint8_t*)p;
+    }
+  }
+  return out_map(sz, false);
 }
 
 void out_release(uint8_t* p, size_t len) {
@@ -143,8 +194,7 @@ void out_release(uint8_t* p, size_t len) {
       return;
     }
   }
-  static const bool reg = getenv("KGS_JS_OUT_REGISTER") != nullptr;
-  if (reg) kgs_host_unregister(p);
+  if (out_registered()) kgs_host_unregister(p);
   munmap(p, sz);
 }
 }  // namespace

@@ -27,6 +27,7 @@ const { poolInfo, diag } = require("../src/backend");
     let [F, T] = mk();
     let proof = await mset_eq_kzg_grandsum_prover(ptau, F, T);  // warm: context, SRS, buffers
     let best = Infinity, bestDiag = null;
+    const all = [], diags = [];
     // fresh standard-form inputs per proof (the prover overwrites them with Montgomery form), all made
     // before the timed loop so the proofs run back to back, as the Python latency probe's do
     const lat = Array.from({ length: proofs }, mk);
@@ -35,6 +36,8 @@ const { poolInfo, diag } = require("../src/backend");
         const t0 = process.hrtime.bigint();
         proof = await mset_eq_kzg_grandsum_prover(ptau, F, T);
         const ms = Number(process.hrtime.bigint() - t0) / 1e6;
+        all.push(+ms.toFixed(3));
+        diags.push([+diag.execMs.toFixed(3)].concat(diag.timing.map(x => +x.toFixed(3))));
         if (ms < best) {
             best = ms;
             bestDiag = { exec_ms: +diag.execMs.toFixed(3), libkgs_timing_ms: diag.timing.map(x => +x.toFixed(3)) };
@@ -43,6 +46,10 @@ const { poolInfo, diag } = require("../src/backend");
     const verified = await mset_eq_kzg_grandsum_verifier(ptau, proof, nBits);
     const out = { nbits: nBits, proofs, ms_per_proof: +best.toFixed(3), proofs_per_s: +(1000 / best).toFixed(3), verified,
                   best_inside_libkgs: bestDiag };
+    if (process.env.KGS_JS_TIME_ALL) {  // every latency sample: [exec_ms, libkgs timing...] each
+        out.all_ms = all;
+        out.all_inside_libkgs = diags;
+    }
     if (conc > 0) {
         // warm every context of the pool (SRS tables are shared per device; buffers are per context)
         await Promise.all(Array.from({ length: conc }, () => { const [a, b] = mk(); return mset_eq_kzg_grandsum_prover(ptau, a, b); }));
