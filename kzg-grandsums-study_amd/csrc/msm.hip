@@ -439,13 +439,10 @@ __device__ __forceinline__ void lo_write_runs(uint32_t* __restrict__ sorted, con
 // one block per (partition, chunk): bases from the partition's chunk histograms, then chunk g of
 // partition p through LDS in tiles of SL_TILE (one tile unless the partition is skewed past SL_G
 // chunks), each bucket's run stored with consecutive lanes (lo_write_runs)
-__global__ void __launch_bounds__(SL_THREADS) __attribute__((amdgpu_waves_per_eu(KGS_SL_WPE, 8))) k_lo_scatter(uint32_t* __restrict__ sorted, uint32_t* __restrict__ offsets,
-                                                           const uint32_t* __restrict__ locnt,
-                                                           const uint32_t* __restrict__ tval,
-                                                           const uint8_t* __restrict__ tlo,
-                                                           const uint32_t* __restrict__ hi_off,
-                                                           const uint32_t* __restrict__ cpre, int NH, int lob) {
-  KGS_AUX_PRIO();
+__device__ __forceinline__ void lo_scatter_body(uint32_t* __restrict__ sorted, uint32_t* __restrict__ offsets,
+                                                const uint32_t* __restrict__ locnt, const uint32_t* __restrict__ tval,
+                                                const uint8_t* __restrict__ tlo, const uint32_t* __restrict__ hi_off,
+                                                const uint32_t* __restrict__ cpre, int NH, int lob) {
   __shared__ uint32_t cur[256], tcnt[256], toff[256], big[256];
   __shared__ uint32_t scp[257], shi[257];
   __shared__ uint32_t sv[SL_TILE];
@@ -526,6 +523,41 @@ __global__ void __launch_bounds__(SL_THREADS) __attribute__((amdgpu_waves_per_eu
     __syncthreads();
     if ((int)tid < nb) cur[tid] += tcnt[tid];
   }
+}
+
+#ifdef KGS_DIAG_CLOCK
+// diagnostic builds only: every k_lo_scatter block appends {offsets pointer (the MSM's context),
+// real-time counter at block start and end, CU id | block index << 32} to a ring, to see how long the
+// workgroups sit resident and when they start relative to each other, alone and in flight
+// (profiles/lo_residency.py; VERDICT r3 Next #4)
+constexpr uint32_t KGS_LOREC_CAP = 1u << 16;
+__device__ unsigned long long g_kgs_lorec[4 * KGS_LOREC_CAP];
+__device__ unsigned int g_kgs_lorec_n;
+#endif
+
+__global__ void __launch_bounds__(SL_THREADS) __attribute__((amdgpu_waves_per_eu(KGS_SL_WPE, 8))) k_lo_scatter(uint32_t* __restrict__ sorted, uint32_t* __restrict__ offsets,
+                                                           const uint32_t* __restrict__ locnt,
+                                                           const uint32_t* __restrict__ tval,
+                                                           const uint8_t* __restrict__ tlo,
+                                                           const uint32_t* __restrict__ hi_off,
+                                                           const uint32_t* __restrict__ cpre, int NH, int lob) {
+  KGS_AUX_PRIO();
+#ifdef KGS_DIAG_CLOCK
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  lo_scatter_body(sorted, offsets, locnt, tval, tlo, hi_off, cpre, NH, lob);
+#ifdef KGS_DIAG_CLOCK
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t slot = atomicAdd(&g_kgs_lorec_n, 1u) % KGS_LOREC_CAP;
+    unsigned long long* o = g_kgs_lorec + 4 * slot;
+    o[0] = (unsigned long long)(uintptr_t)offsets;
+    o[1] = rt0;
+    o[2] = rt1;
+    o[3] = (unsigned long long)__smid() | ((unsigned long long)blockIdx.x << 32);
+  }
+#endif
 }
 
 // ------------------------------------------------------------------ bucket accumulation
@@ -667,6 +699,22 @@ __global__ void __launch_bounds__(256, VW) k_accumulate(uint32_t* __restrict__ s
 }
 
 #ifdef KGS_DIAG_CLOCK
+// k_lo_scatter block records (oldest first when the ring has not wrapped); reset = 1 clears the ring
+extern "C" int kgs_diag_lorec(unsigned long long* out, unsigned int cap, unsigned int* n, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  unsigned int cnt = 0;
+  if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(g_kgs_lorec_n), sizeof(cnt)) != hipSuccess) return 1;
+  const unsigned int have = cnt < KGS_LOREC_CAP ? cnt : KGS_LOREC_CAP;
+  const unsigned int m = have < cap ? have : cap;
+  if (m && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kgs_lorec), 32ull * m) != hipSuccess) return 1;
+  *n = m;
+  if (reset) {
+    const unsigned int z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_kgs_lorec_n), &z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+
 // median over the stamped blocks of d(shader clock) / d(real time) x 100 MHz, in GHz
 extern "C" int kgs_diag_clock(double* ghz, int* nblocks) {
   static unsigned long long h[4 * KGS_CLK_BLOCKS];
