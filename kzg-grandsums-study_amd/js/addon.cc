@@ -8,7 +8,6 @@
 #include <sys/mman.h>
 #include <map>
 #include <chrono>
-#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -106,24 +105,17 @@ constexpr size_t HUGE = (size_t)2 << 20;
 
 size_t out_round(size_t len) { return (len + HUGE - 1) / HUGE * HUGE; }
 
-// KGS_JS_OUT_POOL=N: keep N spare output buffers of each size in use READY — registered
-// (kgs_host_register, so the Montgomery write-back is DMA'd straight into the buffer handed to JS:
-// no pinned staging, no host copy) and already faulted in. A background thread tops the spares up
-// after every allocation, so the registration and first-touch cost is paid beside a proof's GPU work
-// or between proofs instead of inside one; the spares count toward the 2 GiB cache.
-int out_pool_n() {
-  static const int n = getenv("KGS_JS_OUT_POOL") ? atoi(getenv("KGS_JS_OUT_POOL")) : 0;
-  return n > 0 ? n : 0;
-}
 // KGS_JS_OUT_REGISTER=1: pin every output buffer for its life so the write-back is DMA'd in place.
 // Off by default: registering a fresh 32 MiB buffer inside the call costs more than the staging copy
-// it saves whenever the caller keeps its outputs (profiles/r03/boundary_ab.txt); implied by the pool.
+// it saves whenever the caller keeps its outputs (profiles/r03/boundary_ab.txt, profiles/r04/js/). A pool
+// of pre-registered, pre-faulted spares topped up by a background thread was tried too (round 4):
+// no faster, and the thread's registrations kept the process from exiting.
 bool out_registered() {
-  static const bool reg = getenv("KGS_JS_OUT_REGISTER") != nullptr || out_pool_n() > 0;
+  static const bool reg = getenv("KGS_JS_OUT_REGISTER") != nullptr;
   return reg;
 }
 
-uint8_t* out_map(size_t sz, bool prefault) {
+uint8_t* out_map(size_t sz) {
   // over-allocate by one huge page to align the start, then trim the ends
   void* raw = mmap(nullptr, sz + HUGE, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (raw == MAP_FAILED) return nullptr;
@@ -132,8 +124,6 @@ uint8_t* out_map(size_t sz, bool prefault) {
   const uintptr_t end = (uintptr_t)raw + sz + HUGE;
   if (end > a + sz) munmap((void*)(a + sz), end - (a + sz));
   madvise((void*)a, sz, MADV_HUGEPAGE);
-  if (prefault)
-    for (size_t o = 0; o < sz; o += 4096) ((volatile uint8_t*)a)[o] = 0;
   if (out_registered() && kgs_host_register((void*)a, sz) != KGS_OK) {
     munmap((void*)a, sz);
     return nullptr;
@@ -141,39 +131,11 @@ uint8_t* out_map(size_t sz, bool prefault) {
   return (uint8_t*)a;
 }
 
-std::condition_variable g_refill_cv;
-std::vector<size_t> g_refill_req;  // sizes whose spares may need topping up (under g_out_mu)
-
-void refill_loop() {
-  std::unique_lock<std::mutex> lk(g_out_mu);
-  for (;;) {
-    g_refill_cv.wait(lk, [] { return !g_refill_req.empty(); });
-    const size_t sz = g_refill_req.back();
-    g_refill_req.pop_back();
-    while ((int)g_out_free.count(sz) < out_pool_n() && g_out_cached + sz <= OUT_CACHE_MAX) {
-      lk.unlock();
-      uint8_t* p = out_map(sz, true);
-      lk.lock();
-      if (!p) break;
-      g_out_free.emplace(sz, p);
-      g_out_cached += sz;
-    }
-  }
-}
-
-void request_refill(size_t sz) {  // under g_out_mu
-  static std::once_flag once;
-  std::call_once(once, [] { std::thread(refill_loop).detach(); });
-  g_refill_req.push_back(sz);
-  g_refill_cv.notify_one();
-}
-
 uint8_t* out_alloc(size_t len) {
   const size_t sz = out_round(len);
   {
     std::lock_guard<std::mutex> lk(g_out_mu);
     auto it = g_out_free.find(sz);
-    if (out_pool_n() > 0) request_refill(sz);
     if (it != g_out_free.end()) {
       void* p = it->second;
       g_out_free.erase(it);
@@ -181,7 +143,7 @@ uint8_t* out_alloc(size_t len) {
       return (uint8_t*)p;
     }
   }
-  return out_map(sz, false);
+  return out_map(sz);
 }
 
 void out_release(uint8_t* p, size_t len) {
@@ -351,6 +313,8 @@ struct Job {
   bool selected = false;
   bool want_mont = true;  // false: no Montgomery write-back (the other ranks of a distributed proof)
   double exec_ms = 0;     // wall time of job_execute (the libkgs call on the worker thread)
+  // diagnostics: queued (main thread) -> execute start / end (libuv worker) -> complete (main thread)
+  std::chrono::steady_clock::time_point t_queue, t_exec0, t_exec1;
   // proveGroup: rank r's context, SRS slice r of W, one native thread per rank
   std::vector<kgs_ctx_t*> ranks;
   // msmPoints: bases and standard-form scalars (copied: the call returns before the work runs)
@@ -444,10 +408,14 @@ static void group_execute(Job* j) {
 static void job_execute(napi_env, void* data) {
   Job* j = (Job*)data;
   const auto t0 = std::chrono::steady_clock::now();
+  j->t_exec0 = t0;
   struct Stamp {
     Job* j;
     std::chrono::steady_clock::time_point t0;
-    ~Stamp() { j->exec_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+    ~Stamp() {
+      j->t_exec1 = std::chrono::steady_clock::now();
+      j->exec_ms = std::chrono::duration<double, std::milli>(j->t_exec1 - t0).count();
+    }
   } stamp{j, t0};
   if (j->op == 0) {
     j->rc = kgs_srs_load_ptau(j->ctx, j->path.c_str(), j->nbits_max);
@@ -528,6 +496,16 @@ static void job_complete(napi_env env, napi_status, void* data) {
     napi_value ems;
     napi_create_double(env, j->exec_ms, &ems);
     napi_set_named_property(env, o, "execMs", ems);  // diagnostics: time inside libkgs
+    // diagnostics: [queued -> worker start, worker end -> this completion callback] in ms
+    const auto tc = std::chrono::steady_clock::now();
+    napi_create_array(env, &arr);
+    const double d0 = std::chrono::duration<double, std::milli>(j->t_exec0 - j->t_queue).count();
+    const double d1 = std::chrono::duration<double, std::milli>(tc - j->t_exec1).count();
+    napi_create_double(env, d0, &ems);
+    napi_set_element(env, arr, 0, ems);
+    napi_create_double(env, d1, &ems);
+    napi_set_element(env, arr, 1, ems);
+    napi_set_named_property(env, o, "waitMs", arr);
     j->mf.clear();
     j->mt.clear();
     napi_resolve_deferred(env, j->deferred, o);
@@ -548,6 +526,7 @@ static napi_value queue(napi_env env, Job* j, const char* name) {
   NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
   napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &rname);
   NAPI_CALL(env, napi_create_async_work(env, nullptr, rname, job_execute, job_complete, j, &j->work));
+  j->t_queue = std::chrono::steady_clock::now();
   NAPI_CALL(env, napi_queue_async_work(env, j->work));
   if (j->op == 1 || j->op == 3) flush_external(env);  // a GC it starts now runs beside the proof just queued
   return promise;

@@ -42,7 +42,7 @@ function perDevice() {
 }
 
 const pool = { slots: [], idle: [], waiters: [], devs: null, cap: 0 };
-const diag = { execMs: null, timing: null };
+const diag = { execMs: null, timing: null, waitMs: null, callMs: null };
 
 function newSlot() {
     if (!pool.devs) {
@@ -128,8 +128,12 @@ async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT) {
             slot.srsBits = nBits;
         }
         setLanes(slot);
+        const t0 = process.hrtime.bigint();
         const res = await load().prove(slot.ctx, kind, nBits, evalsF, evalsT, selF, selT);
-        // diagnostics of the last call (time inside libkgs; kgs_last_timing rounds / copy / prover / write-back)
+        // diagnostics of the last call: the native call's wall time, its [queue -> worker, worker ->
+        // completion] waits, time inside libkgs, kgs_last_timing rounds / copy / prover / write-back
+        diag.callMs = Number(process.hrtime.bigint() - t0) / 1e6;
+        diag.waitMs = res.waitMs;
         diag.execMs = res.execMs;
         diag.timing = load().lastTiming(slot.ctx);
         return res;

@@ -27,7 +27,7 @@ const { poolInfo, diag } = require("../src/backend");
     let [F, T] = mk();
     let proof = await mset_eq_kzg_grandsum_prover(ptau, F, T);  // warm: context, SRS, buffers
     let best = Infinity, bestDiag = null;
-    const all = [], diags = [];
+    const all = [], diags = [], calls = [];
     // fresh standard-form inputs per proof (the prover overwrites them with Montgomery form), all made
     // before the timed loop so the proofs run back to back, as the Python latency probe's do
     const lat = Array.from({ length: proofs }, mk);
@@ -38,6 +38,7 @@ const { poolInfo, diag } = require("../src/backend");
         const ms = Number(process.hrtime.bigint() - t0) / 1e6;
         all.push(+ms.toFixed(3));
         diags.push([+diag.execMs.toFixed(3)].concat(diag.timing.map(x => +x.toFixed(3))));
+        calls.push([+diag.callMs.toFixed(3)].concat(diag.waitMs.map(x => +x.toFixed(3))));
         if (ms < best) {
             best = ms;
             bestDiag = { exec_ms: +diag.execMs.toFixed(3), libkgs_timing_ms: diag.timing.map(x => +x.toFixed(3)) };
@@ -49,6 +50,7 @@ const { poolInfo, diag } = require("../src/backend");
     if (process.env.KGS_JS_TIME_ALL) {  // every latency sample: [exec_ms, libkgs timing...] each
         out.all_ms = all;
         out.all_inside_libkgs = diags;
+        out.all_native_call = calls;  // [native call wall ms, queue -> worker ms, worker -> completion ms]
     }
     if (conc > 0) {
         // warm every context of the pool (SRS tables are shared per device; buffers are per context)
