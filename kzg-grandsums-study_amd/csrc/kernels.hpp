@@ -56,6 +56,9 @@ struct MsmWork {
 };
 
 // ntt.hip
+// NTT LDS passes built for three waves per SIMD (co-resident with two accumulate waves: proofs in
+// flight) or two (fastest alone) for the calling thread's later launches; returns the previous setting
+bool ntt_set_coresident(bool on);
 void ntt_dif(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t in_len, int logm, const uint32_t* pre,
              const uint32_t* tw, int logM);
 void ntt_dit(hipStream_t st, uint32_t* out, const uint32_t* in, int in_bitrev, int logm, const uint32_t* tw, int logM,

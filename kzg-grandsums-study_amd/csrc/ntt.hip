@@ -425,26 +425,31 @@ __device__ __forceinline__ void lds_round_all(uint32_t* lds, const uint32_t* __r
 // K1 + K2 + K3 stages from s0 (two or three register rounds with an LDS exchange between rounds).
 // DIRECT: the first round loads from and the last round stores to global memory (d >= LB); else the
 // tile is loaded into / stored from LDS in address order around the rounds.
-// A/B knob: the passes' register budget as waves per SIMD (KGS_NTT_WAVES=3: <= 168 VGPRs + AGPRs, so
-// one pass wave fits beside two resident accumulate waves per SIMD, 2 x 168 + 168 <= 512)
-#ifdef KGS_NTT_WAVES
-#define KGS_NTT_VGPR_ATTR __attribute__((amdgpu_waves_per_eu(KGS_NTT_WAVES)))
-#else
-#define KGS_NTT_VGPR_ATTR
-#endif
-template <int K1, int K2, int K3, bool DIT, bool DIRECT>
-__global__ void __launch_bounds__(LDS_NT) KGS_NTT_VGPR_ATTR k_ntt_lds_pass(ntt_io io, const uint32_t* __restrict__ tw, int s0) {
+// WV = the waves per SIMD the pass is compiled for. WV = 2 (211 VGPRs for the 9-stage DIF pass): the
+// fastest pass alone, but a pass wave cannot start on a SIMD that holds two accumulate waves (2 x 168
+// + 211 > 512), so in flight the other proofs' NTT blocks wait for a CU's accumulate blocks to drain.
+// WV = 3 (<= 168 VGPRs: 2 x 168 + 168 <= 512; the DIF passes spill 100-164 B): 9 % slower alone
+// (2^21 pair 0.56 vs 0.515 ms) and +0.6 % proofs/s with four proofs in flight, higher than the
+// WV = 2 build in all 5 same-box reps on two boxes (profiles/r04/coresidency/, profiles/r04/ntt/).
+// Contexts proving one proof at a time (two MSM lanes, the latency mode) and every other caller
+// launch WV = 2; in-flight contexts (one lane) WV = 3 (ntt_set_coresident).
+template <int K1, int K2, int K3, bool DIT, bool DIRECT, int WV>
+__global__ void __launch_bounds__(LDS_NT) __attribute__((amdgpu_waves_per_eu(WV, WV)))
+k_ntt_lds_pass(ntt_io io, const uint32_t* __restrict__ tw, int s0) {
   KGS_AUX_PRIO();
   constexpr int K = K1 + K2 + K3;
   constexpr int LBLOG = NTT_ELOG - K;
   constexpr int LB = 1 << LBLOG;
-#ifdef KGS_NTT_WAVES
-  // dynamic LDS: with a static 64 KiB tile the compiler takes the LDS-bound occupancy (2 blocks per CU)
-  // as the target and ignores waves_per_eu
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-#else
-  __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_ELEMS * 8];
-#endif
+  uint32_t* lds;
+  if constexpr (WV >= 3) {
+    // dynamic LDS: with a static 64 KiB tile the compiler takes the LDS-bound occupancy (2 blocks per
+    // CU) as its target and ignores waves_per_eu
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
+    lds = lds_dyn;
+  } else {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_tile[LDS_ELEMS * 8];
+    lds = lds_tile;
+  }
   const int logd = DIT ? s0 : io.logm - s0 - K;
   const uint32_t col0 = blockIdx.x * LB;
   if (!DIRECT) {  // load (address order)
@@ -475,6 +480,9 @@ __global__ void __launch_bounds__(LDS_NT) KGS_NTT_VGPR_ATTR k_ntt_lds_pass(ntt_i
   }
 }
 
+// the calling thread's pass build (ntt_set_coresident; per thread: contexts prove on their callers' threads)
+thread_local bool g_ntt_coresident = false;
+
 #ifndef KGS_NO_NTT_LDS
 // LDS passes need m >= the tile (2^NTT_ELOG elements)
 constexpr int LDS_MIN_LOGM = NTT_ELOG > 11 ? NTT_ELOG : 11;
@@ -499,12 +507,6 @@ static int lds_plan(int logm, int* ks) {
   return P;
 }
 
-#ifdef KGS_NTT_WAVES
-constexpr unsigned NTT_DYN_LDS = LDS_ELEMS * 32;
-#else
-constexpr unsigned NTT_DYN_LDS = 0;
-#endif
-
 static void launch_lds_pass(hipStream_t st, int K, bool dit, uint32_t* data, const uint32_t* in, uint64_t in_len,
                             int in_bitrev, const uint32_t* pre, const uint32_t* tw, int logm, int s0,
                             const uint32_t* post, const uint32_t* post_s) {
@@ -513,8 +515,14 @@ static void launch_lds_pass(hipStream_t st, int K, bool dit, uint32_t* data, con
   const int logd = dit ? s0 : logm - s0 - K;
   static const bool staged = getenv("KGS_NTT_STAGED") != nullptr;  // A/B: every pass staged through LDS
   const bool direct = logd >= NTT_ELOG - K && !staged;
-#define KGS_LDS_LAUNCH(A, B, C, D, E) \
-  hipLaunchKernelGGL((k_ntt_lds_pass<A, B, C, D, E>), dim3(blocks), dim3(LDS_NT), NTT_DYN_LDS, st, io, tw, s0)
+#define KGS_LDS_LAUNCH(A, B, C, D, E)                                                                          \
+  do {                                                                                                         \
+    if (g_ntt_coresident)                                                                                      \
+      hipLaunchKernelGGL((k_ntt_lds_pass<A, B, C, D, E, 3>), dim3(blocks), dim3(LDS_NT), LDS_ELEMS * 32, st, io, \
+                         tw, s0);                                                                              \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_ntt_lds_pass<A, B, C, D, E, 2>), dim3(blocks), dim3(LDS_NT), 0, st, io, tw, s0);   \
+  } while (0)
 #define KGS_LDS_BY_K(D, E)                          \
   switch (K) {                                      \
     case 9: KGS_LDS_LAUNCH(3, 3, 3, D, E); break;   \
@@ -541,6 +549,12 @@ static void launch_lds_pass(hipStream_t st, int K, bool dit, uint32_t* data, con
 #undef KGS_LDS_LAUNCH
 }
 #endif
+
+bool ntt_set_coresident(bool on) {
+  const bool prev = g_ntt_coresident;
+  g_ntt_coresident = on;
+  return prev;
+}
 
 void ntt_dif(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t in_len, int logm,
              const uint32_t* pre, const uint32_t* tw, int logM) {

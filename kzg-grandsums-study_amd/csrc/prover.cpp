@@ -589,6 +589,13 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     prove_dist_group(c, in, com_out, ev_out);
     return;
   }
+  // in-flight contexts (one MSM lane) launch the NTT passes built to co-reside with the other proofs'
+  // accumulate waves, the latency mode (two lanes) the build that is fastest alone (ntt.hip, WV)
+  struct NttMode {
+    bool prev;
+    explicit NttMode(bool on) : prev(ntt_set_coresident(on)) {}
+    ~NttMode() { ntt_set_coresident(prev); }
+  } ntt_mode(c.msm_lanes < 2);
   using clk = std::chrono::steady_clock;
   auto t0 = clk::now();
   c.timing.resize(9, 0.0);

@@ -7,7 +7,7 @@ set -e
 cd "$(dirname "$0")/../.."
 R=$PWD
 OUT=$R/gpurun_out/js
-bash profiles/r04/run_js.sh
+mkdir -p $OUT
 for L in lib lib_ab/ntt3w lib_ab/mac4 lib lib_ab/ntt3w lib_ab/mac4; do
   KGS_LIB=$R/kzg-grandsums-study_amd/$L/libkgs.so timeout -k 10 120 python3 profiles/ntt_ab.py 21 50 >> $OUT/ntt_alone.txt 2>&1
 done
@@ -18,3 +18,4 @@ KGS_LIB=$R/kzg-grandsums-study_amd/lib_diag/libkgs.so timeout -k 10 300 python3 
 grep -v amdgpu.ids $OUT/lo_residency.txt
 timeout -k 10 900 python3 profiles/ab_bench.py 3 kzg-grandsums-study_amd/lib/libkgs.so kzg-grandsums-study_amd/lib_ab/ntt3w/libkgs.so kzg-grandsums-study_amd/lib_ab/mac4/libkgs.so > $OUT/ntt_bench_ab.txt 2>&1 || { cat $OUT/ntt_bench_ab.txt; exit 1; }
 cat $OUT/ntt_bench_ab.txt
+bash profiles/r04/run_js.sh
