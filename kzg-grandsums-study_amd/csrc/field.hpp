@@ -234,37 +234,6 @@ struct Fe {
         : "+v"(accA), "=&v"(tA), "+v"(accB), "=&v"(tB), "=&s"(cA0), "=&s"(cB0), "=&s"(cA1), "=&s"(cB1)
         : "v"(xA0), "v"(yA0), "v"(xA1), "v"(yA1), "v"(xB0), "v"(yB0), "v"(xB1), "v"(yB1));
   }
-#ifdef KGS_MAC4
-  // four terms of one column of each product in ONE asm block: half the asm boundaries of mac2_x2
-  // (the compiler pads each boundary after a carry-writing VALU with an s_nop: ~1,500 per NTT pass)
-  __device__ __forceinline__ static void mac4_x2(uint64_t& accA, uint32_t& tA, const uint32_t (&xA)[4],
-                                                 const uint32_t (&yA)[4], uint64_t& accB, uint32_t& tB,
-                                                 const uint32_t (&xB)[4], const uint32_t (&yB)[4]) {
-    uint64_t cA0, cB0, cA1, cB1, cA2, cB2, cA3, cB3;
-    asm("v_mad_u64_u32 %0, %4, %12, %13, %0\n\tv_mad_u64_u32 %2, %5, %20, %21, %2\n\t"
-        "v_addc_co_u32 %1, %4, 0, %1, %4\n\tv_addc_co_u32 %3, %5, 0, %3, %5\n\t"
-        "v_mad_u64_u32 %0, %6, %14, %15, %0\n\tv_mad_u64_u32 %2, %7, %22, %23, %2\n\t"
-        "v_addc_co_u32 %1, %6, 0, %1, %6\n\tv_addc_co_u32 %3, %7, 0, %3, %7\n\t"
-        "v_mad_u64_u32 %0, %8, %16, %17, %0\n\tv_mad_u64_u32 %2, %9, %24, %25, %2\n\t"
-        "v_addc_co_u32 %1, %8, 0, %1, %8\n\tv_addc_co_u32 %3, %9, 0, %3, %9\n\t"
-        "v_mad_u64_u32 %0, %10, %18, %19, %0\n\tv_mad_u64_u32 %2, %11, %26, %27, %2\n\t"
-        "v_addc_co_u32 %1, %10, 0, %1, %10\n\tv_addc_co_u32 %3, %11, 0, %3, %11"
-        : "+v"(accA), "+v"(tA), "+v"(accB), "+v"(tB), "=&s"(cA0), "=&s"(cB0), "=&s"(cA1), "=&s"(cB1), "=&s"(cA2),
-          "=&s"(cB2), "=&s"(cA3), "=&s"(cB3)
-        : "v"(xA[0]), "v"(yA[0]), "v"(xA[1]), "v"(yA[1]), "v"(xA[2]), "v"(yA[2]), "v"(xA[3]), "v"(yA[3]), "v"(xB[0]),
-          "v"(yB[0]), "v"(xB[1]), "v"(yB[1]), "v"(xB[2]), "v"(yB[2]), "v"(xB[3]), "v"(yB[3]));
-  }
-  // the terms (a_j b_k, m_j p_k) for j = j0, j0 + 1 (k = i - j) of both products
-  __device__ __forceinline__ static void col4_x2(uint64_t& acc, uint32_t& ta, const uint32_t* a, const uint32_t* b,
-                                                 const uint32_t* m, uint64_t& acd, uint32_t& tc, const uint32_t* c,
-                                                 const uint32_t* d, const uint32_t* n, int i, int j0) {
-    const uint32_t xA[4] = {a[j0], m[j0], a[j0 + 1], m[j0 + 1]};
-    const uint32_t yA[4] = {b[i - j0], P::p[i - j0], b[i - j0 - 1], P::p[i - j0 - 1]};
-    const uint32_t xB[4] = {c[j0], n[j0], c[j0 + 1], n[j0 + 1]};
-    const uint32_t yB[4] = {d[i - j0], P::p[i - j0], d[i - j0 - 1], P::p[i - j0 - 1]};
-    mac4_x2(acc, ta, xA, yA, acd, tc, xB, yB);
-  }
-#endif
   // RA = A*B*R^-1, RB = C*D*R^-1, each in [0, 2p) for inputs in [0, 2p): mul_nored twice, interleaved.
   // The outputs must not alias the inputs (mul_nored_x2_ip for X *= B, Y *= D).
   __device__ __forceinline__ static void mul_nored_x2(const Fe& A, const Fe& B, const Fe& C, const Fe& D, Fe& RA,
@@ -279,13 +248,8 @@ struct Fe {
         mac_x2_init(acc, ta, a[0], b[0], acd, tc, c[0], d[0]);
       } else {
         mac2_x2_init(acc, ta, a[0], b[i], m[0], P::p[i], acd, tc, c[0], d[i], n[0], P::p[i]);
-        int j = 1;
-#ifdef KGS_MAC4
 #pragma unroll
-        for (; j + 1 < i; j += 2) col4_x2(acc, ta, a, b, m, acd, tc, c, d, n, i, j);
-#endif
-#pragma unroll
-        for (; j < i; j++)
+        for (int j = 1; j < i; j++)
           mac2_x2(acc, ta, a[j], b[i - j], m[j], P::p[i - j], acd, tc, c[j], d[i - j], n[j], P::p[i - j]);
         mac_x2(acc, ta, a[i], b[0], acd, tc, c[i], d[0]);
       }
@@ -298,13 +262,8 @@ struct Fe {
 #pragma unroll
     for (int i = 8; i < 15; i++) {
       mac2_x2_init(acc, ta, a[i - 7], b[7], m[i - 7], P::p[7], acd, tc, c[i - 7], d[7], n[i - 7], P::p[7]);
-      int j = i - 6;
-#ifdef KGS_MAC4
 #pragma unroll
-      for (; j + 1 < 8; j += 2) col4_x2(acc, ta, a, b, m, acd, tc, c, d, n, i, j);
-#endif
-#pragma unroll
-      for (; j < 8; j++)
+      for (int j = i - 6; j < 8; j++)
         mac2_x2(acc, ta, a[j], b[i - j], m[j], P::p[i - j], acd, tc, c[j], d[i - j], n[j], P::p[i - j]);
       RA.v[i - 8] = (uint32_t)acc;
       RB.v[i - 8] = (uint32_t)acd;
