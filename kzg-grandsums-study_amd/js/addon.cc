@@ -2,7 +2,6 @@
 // JavaScript drop-in modules in js/src. Heavy calls (SRS load, prove) run in napi_async_work and
 // return Promises, like the reference's async module API.
 #include <node_api.h>
-#include <v8.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -293,7 +292,6 @@ static napi_value SrsInfo(napi_env env, napi_callback_info info) {
 }
 
 // ---------------------------------------------------------------- async work
-static int g_proofs_in_flight = 0;  // prove / proveGroup jobs queued and not completed (main thread)
 struct Job {
   napi_async_work work = nullptr;
   napi_deferred deferred = nullptr;
@@ -461,7 +459,6 @@ static void job_execute(napi_env, void* data) {
 
 static void job_complete(napi_env env, napi_status, void* data) {
   Job* j = (Job*)data;
-  if (j->op == 1 || j->op == 3) g_proofs_in_flight--;
   if (j->rc != KGS_OK) {
     napi_value msg, err, code;
     napi_create_string_utf8(env, j->err.c_str(), NAPI_AUTO_LENGTH, &msg);
@@ -524,20 +521,6 @@ static void job_complete(napi_env env, napi_status, void* data) {
   delete j;
 }
 
-// Eager collection beside a lone proof. Each proof leaves its callers' previous input buffers (the
-// reference replaces Evaluations.eval by the Montgomery copy, prover.js:147-148) as 64 MiB of garbage
-// at n = 2^20, and V8 then finalises a mark-sweep of ~6 ms as a main-thread task that, scheduled
-// while the GPU works, used to land just as the proof completed: the Promise resolved 1-8 ms after
-// the result was ready (profiles/r04/js/). With no other proof in flight the full collection is run
-// right after the proof is queued, beside its ~15 ms of GPU work. KGS_JS_EAGER_GC=0 turns it off.
-static bool eager_gc() {
-  static const bool on = [] {
-    const char* e = getenv("KGS_JS_EAGER_GC");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 static napi_value queue(napi_env env, Job* j, const char* name) {
   napi_value promise, rname;
   NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
@@ -545,10 +528,7 @@ static napi_value queue(napi_env env, Job* j, const char* name) {
   NAPI_CALL(env, napi_create_async_work(env, nullptr, rname, job_execute, job_complete, j, &j->work));
   j->t_queue = std::chrono::steady_clock::now();
   NAPI_CALL(env, napi_queue_async_work(env, j->work));
-  if (j->op == 1 || j->op == 3) {
-    flush_external(env);  // a GC it starts now runs beside the proof just queued
-    if (++g_proofs_in_flight == 1 && eager_gc()) v8::Isolate::GetCurrent()->LowMemoryNotification();
-  }
+  if (j->op == 1 || j->op == 3) flush_external(env);  // a GC it starts now runs beside the proof just queued
   return promise;
 }
 

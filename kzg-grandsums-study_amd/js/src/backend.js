@@ -80,6 +80,29 @@ async function withContext(fn) {
     }
 }
 
+// Eager collection beside a lone proof. Every proof leaves the caller's previous input buffers (the
+// reference replaces Evaluations.eval by the Montgomery copy, prover.js:147-148) as 64 MiB of garbage
+// at n = 2^20; V8 then finalises a ~6 ms mark-sweep as a main-thread task, which, scheduled while the
+// GPU works, tended to run just as the proof completed: the Promise resolved 0.1-5 ms after the
+// result was ready (profiles/r04/js/). A proof alone on its device therefore runs one full collection
+// right after it is queued, beside its ~15 ms of GPU work; with other proofs in flight V8's own
+// schedule is kept. KGS_JS_EAGER_GC=0 turns it off.
+let gcFn;
+function collectNow() {
+    if (gcFn === undefined) {
+        gcFn = null;
+        if (process.env.KGS_JS_EAGER_GC !== "0") {
+            try {
+                require("v8").setFlagsFromString("--expose_gc");
+                gcFn = require("vm").runInNewContext("gc");
+            } catch (e) {
+                gcFn = null;
+            }
+        }
+    }
+    if (gcFn) gcFn();
+}
+
 // MSM lanes of a proof about to start: two (single-proof latency mode, kgs_ctx_set_msm_lanes) when it
 // is alone on its device, one when other proofs are in flight there or waiting for a context — the
 // GPU is then already full, and the two-lane accumulation's register reservation would keep the
@@ -129,7 +152,9 @@ async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT) {
         }
         setLanes(slot);
         const t0 = process.hrtime.bigint();
-        const res = await load().prove(slot.ctx, kind, nBits, evalsF, evalsT, selF, selT);
+        const pending = load().prove(slot.ctx, kind, nBits, evalsF, evalsT, selF, selT);
+        if (slot.lanes === 2) collectNow();  // alone on its device: see collectNow
+        const res = await pending;
         // diagnostics of the last call: the native call's wall time, its [queue -> worker, worker ->
         // completion] waits, time inside libkgs, kgs_last_timing rounds / copy / prover / write-back
         diag.callMs = Number(process.hrtime.bigint() - t0) / 1e6;
