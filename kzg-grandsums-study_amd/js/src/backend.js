@@ -86,7 +86,18 @@ async function withContext(fn) {
 // GPU works, tended to run just as the proof completed: the Promise resolved 0.1-5 ms after the
 // result was ready (profiles/r04/js/). A proof alone on its device therefore runs one full collection
 // right after it is queued, beside its ~15 ms of GPU work; with other proofs in flight V8's own
-// schedule is kept. KGS_JS_EAGER_GC=0 turns it off.
+// schedule is kept. The collection is started GC_DELAY_MS after the proof is queued: freeing the
+// garbage's pages while round 1 copies the next inputs into pinned staging stretched that round from
+// 3.4 to 9-15 ms in a third of the samples (profiles/r04/js/run5). KGS_JS_EAGER_GC=0 turns it off,
+// KGS_JS_EAGER_GC=<ms> sets the delay.
+const GC_DELAY_MS = (() => {
+    const v = parseInt(process.env.KGS_JS_EAGER_GC || "", 10);
+    return Number.isFinite(v) && v > 1 ? v : 5;
+})();
+function scheduleCollect() {
+    if (process.env.KGS_JS_EAGER_GC === "0") return;
+    setTimeout(collectNow, GC_DELAY_MS);
+}
 let gcFn;
 function collectNow() {
     if (gcFn === undefined) {
@@ -153,7 +164,7 @@ async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT) {
         setLanes(slot);
         const t0 = process.hrtime.bigint();
         const pending = load().prove(slot.ctx, kind, nBits, evalsF, evalsT, selF, selT);
-        if (slot.lanes === 2) collectNow();  // alone on its device: see collectNow
+        if (slot.lanes === 2) scheduleCollect();  // alone on its device: see collectNow
         const res = await pending;
         // diagnostics of the last call: the native call's wall time, its [queue -> worker, worker ->
         // completion] waits, time inside libkgs, kgs_last_timing rounds / copy / prover / write-back
