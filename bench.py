@@ -437,10 +437,10 @@ def main():
         js_dir = os.path.join(HERE, "kzg-grandsums-study_amd", "js")
         if shutil.which("node") and os.path.exists(os.path.join(js_dir, "build", "kgs_addon.node")):
             try:
-                # latency: best of 3 one-at-a-time proofs; throughput: 16 concurrent chains of 3
+                # latency: best of 5 one-at-a-time proofs; throughput: 16 concurrent chains of 5
                 # awaited prover() calls over the module's context pool (8 contexts on this GPU)
                 env = dict(os.environ, KGS_JS_CONTEXTS=str(2 * args.inflight), KGS_DEVICES=str(local))
-                out = subprocess.run(["node", os.path.join(js_dir, "test", "time_prove.js"), ptau, str(nbits), "3",
+                out = subprocess.run(["node", os.path.join(js_dir, "test", "time_prove.js"), ptau, str(nbits), "5",
                                       str(4 * args.inflight)], capture_output=True, text=True, timeout=300, env=env)
                 host_leg["javascript_module"] = json.loads(out.stdout.strip().splitlines()[-1])
             except Exception as e:  # the JS leg must not hide the GPU number
