@@ -351,7 +351,9 @@ def test_large_proof_properties(K, kind, nbits, npols, sel):
 @pytest.mark.parametrize("kind,nbits,npols,sel", [("grandsum", 14, 1, False), ("grandproduct", 14, 1, False),
                                                   ("grandsum", 13, 2, True), ("grandproduct", 13, 3, True)])
 def test_mid_size_vs_c_oracle(K, kind, nbits, npols, sel):
-    """Byte-for-byte against the C restatement at sizes the Python oracle is too slow for."""
+    """Byte-for-byte against the C restatement at sizes the Python oracle is too slow for, in both
+    context modes: two MSM lanes (one proof at a time; NTT passes built for 2 waves/SIMD) and one lane
+    (proofs in flight; NTT passes built for 3 waves/SIMD, ntt.hip)."""
     from oracle import cbackend as C
     path = f"/tmp/kgs_test_gpu_p{nbits}.ptau"
     ctx = K.Context(0)
@@ -360,10 +362,12 @@ def test_mid_size_vs_c_oracle(K, kind, nbits, npols, sel):
     ctx.load_ptau(path, nbits)
     Fs, Ts, sF, sT = common.make_inputs(nbits * 3 + npols, nbits, npols, sel)
     kk = K.GRANDSUM if kind == "grandsum" else K.GRANDPRODUCT
-    coms, evs, _, _ = ctx.prove(kk, nbits, Fs, Ts, sF, sT, mont_out=False)
     _, srs = C.load_srs_bytes(path)
     ecoms, eevs = C.prove_raw(kk, nbits, Fs, Ts, sF, sT, srs, 0)
-    assert coms == ecoms and evs == eevs
+    for lanes in (2, 1):
+        ctx.set_msm_lanes(lanes)
+        coms, evs, _, _ = ctx.prove(kk, nbits, Fs, Ts, sF, sT, mont_out=False)
+        assert coms == ecoms and evs == eevs, lanes
     ctx.close()
 
 
