@@ -779,14 +779,22 @@ __global__ void __launch_bounds__(256) k_combine_level(uint32_t* __restrict__ ra
   if (list_out) combine_enqueue(list_out, cnt_out, s, o0, o1, L, stride * CB_T);
 }
 
-// bucket b's total replaces its start record (run_rec b), for every b in 1..B (empty: infinity)
+// bucket b's total replaces its start record (run_rec b), for every b in 1..B (empty: infinity).
+// KGS_COMBINE_LANES threads per bucket split its partials and add their sums with one shuffle (2), or
+// one thread walks them all (1).
+#ifndef KGS_COMBINE_LANES
+#define KGS_COMBINE_LANES 2
+#endif
+constexpr uint32_t COMBINE_LANES = KGS_COMBINE_LANES;
+static_assert(COMBINE_LANES == 1 || COMBINE_LANES == 2, "k_combine lanes per bucket");
 __global__ void __launch_bounds__(256) k_combine(uint32_t* __restrict__ raw, uint32_t nbins,
                                                  const uint32_t* __restrict__ offsets, uint32_t B, uint32_t L,
                                                  uint64_t stride) {
   KGS_AUX_PRIO();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t b = (g >> 1) + 1;  // buckets 1..B
-  const uint32_t sub = g & 1;
+  const uint32_t b = g / COMBINE_LANES + 1;  // buckets 1..B
+  const uint32_t sub = g % COMBINE_LANES;
+  if (COMBINE_LANES == 1 && b > B) return;
   g1_acc29 acc;
   acc.set_inf();
   if (b <= B) {
@@ -795,11 +803,11 @@ __global__ void __launch_bounds__(256) k_combine(uint32_t* __restrict__ raw, uin
       if (sub == 0) acc = g1_acc29::load_raw(run_rec(raw, b));
       const uint64_t s_lo = o0 / L + 1, s_hi = (o1 + L - 1) / L;
       const uint64_t st = s_hi > s_lo + CB_T ? stride : 1;  // reduced by the levels, or short
-      for (uint64_t sgm = s_lo + sub * st; sgm < s_hi; sgm += 2 * st)
+      for (uint64_t sgm = s_lo + sub * st; sgm < s_hi; sgm += COMBINE_LANES * st)
         acc.add(g1_acc29::load_raw(run_rec(raw, nbins + sgm)));
     }
   }
-  acc.add(shfl_xor_acc(acc, 1));
+  if (COMBINE_LANES == 2) acc.add(shfl_xor_acc(acc, 1));
   if (b <= B && sub == 0) acc.store_raw(run_rec(raw, b));
 }
 
@@ -940,7 +948,7 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
                        cnt + j, lout, lout ? cnt + j + 1 : nullptr, (uint32_t)L, stride);
     cap = cap / CB_T + B + 16;
   }
-  hipLaunchKernelGGL(k_combine, dim3(nb(2 * (uint64_t)B)), dim3(256), 0, st, w.raw29, B + 1, w.offsets, B,
+  hipLaunchKernelGGL(k_combine, dim3(nb(COMBINE_LANES * (uint64_t)B)), dim3(256), 0, st, w.raw29, B + 1, w.offsets, B,
                      (uint32_t)L, stride);
   if (ev) hipEventRecord(ev[3], st);
   // row / column sums (2^h + 2^l blocks), then the c bit sums
