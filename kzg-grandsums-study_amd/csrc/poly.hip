@@ -460,15 +460,20 @@ __global__ void __launch_bounds__(256) k_eval_tiles(uint32_t* __restrict__ part,
     fr ci = i < len ? fr::load(c + 8 * i) : fr::zero();
     h = h * x + ci;
   }
-  // tree: thread t (multiple of 2^(l+1)) absorbs t + 2^l scaled by x^(8*2^l)
-  for (int l = 0; l < 8; l++) {
-    h.store(lds + 8 * threadIdx.x);
+  // tree over the 256 partials, level l combining the previous level's pairs (2k, 2k+1) as
+  // v_2k + v_2k+1 * x^(8*2^l) in threads k < 128 >> l: the active threads are contiguous, so whole
+  // waves drop out (9 wave-products for the tree instead of 27 when thread t of every stride ran)
+  h.store(lds + 8 * threadIdx.x);
+  __syncthreads();
+  for (int l = 0, cnt = 128; l < 8; l++, cnt >>= 1) {
+    const bool on = (int)threadIdx.x < cnt;
+    fr v;
+    if (on) v = fr::load(lds + 8 * (2 * threadIdx.x)) + fr::load(lds + 8 * (2 * threadIdx.x + 1)) * fr::load(xp + 8 * l);
     __syncthreads();
-    const int span = 1 << l;
-    if ((threadIdx.x & (2 * span - 1)) == 0) h = h + fr::load(lds + 8 * (threadIdx.x + span)) * fr::load(xp + 8 * l);
+    if (on) v.store(lds + 8 * threadIdx.x);
     __syncthreads();
   }
-  if (threadIdx.x == 0) h.store(part + 8 * ((uint64_t)pi * ntiles_max + blockIdx.x));
+  if (threadIdx.x == 0) fr::load(lds).store(part + 8 * ((uint64_t)pi * ntiles_max + blockIdx.x));
 }
 
 void launch_eval_tiles(hipStream_t st, uint32_t* part, const EvalBatch& eb, const uint32_t* xp, uint32_t ntiles_max) {
