@@ -780,10 +780,12 @@ __global__ void __launch_bounds__(256) k_combine_level(uint32_t* __restrict__ ra
 }
 
 // bucket b's total replaces its start record (run_rec b), for every b in 1..B (empty: infinity).
-// KGS_COMBINE_LANES threads per bucket split its partials and add their sums with one shuffle (2), or
-// one thread walks them all (1).
+// KGS_COMBINE_LANES threads per bucket: one thread walks the bucket's partials (1, default), or two
+// split them and add their sums with one shuffle (2). A bucket has 2-3 partials at 2^20 points; two
+// lanes ran ~6 wave-adds per 64 buckets against ~4 for one lane: +0.7 % proofs/s in 3 of 3 same-box
+// reps, combine 0.057 -> 0.053 ms alone, skewed MSMs unchanged (profiles/r04/comb/).
 #ifndef KGS_COMBINE_LANES
-#define KGS_COMBINE_LANES 2
+#define KGS_COMBINE_LANES 1
 #endif
 constexpr uint32_t COMBINE_LANES = KGS_COMBINE_LANES;
 static_assert(COMBINE_LANES == 1 || COMBINE_LANES == 2, "k_combine lanes per bucket");
