@@ -739,7 +739,7 @@ extern "C" int kgs_diag_clock(double* ghz, int* nblocks) {
 // lands in the same bucket of each window), so the partials are first reduced in CB_LEVELS chunked
 // levels: at level j the thread of segment s = s_lo + i*CB_T^(j+1) adds the CB_T partials at stride
 // CB_T^j that follow it (in place). The final pass then has <= ceil(m / CB_T^CB_LEVELS) partials per
-// bucket, two lanes per bucket joined by one xor-shuffle add. Depth for m partials:
+// bucket, walked by one lane (KGS_COMBINE_LANES). Depth for m partials:
 // ~CB_T*CB_LEVELS + m/CB_T^3. Lists of <= CB_T partials (every bucket of a uniform scalar
 // distribution) skip the levels. All of the tail (combine, bit sums) adds run records in the fq29
 // form with g1_acc29::add; only the c bit sums leave as 256-bit XYZZ points for the host.
@@ -851,6 +851,32 @@ __global__ void __launch_bounds__(256) k_rowcol(uint32_t* __restrict__ rc, const
   if (t == 0) v.store_raw(rc + (uint64_t)RAW29_WORDS * r);
 }
 
+// The same row / column sums with 16 lanes per line (4 lines per wave): each lane adds its 1/16 of
+// the line sequentially, then 4 xor-shuffle levels. 4.75 wave-adds per line instead of the block
+// tree's 9 (whose levels leave most lanes of their waves idle), at 19 dependent adds instead of 9:
+// the in-flight build (other proofs fill the latency); one proof at a time keeps k_rowcol.
+constexpr uint32_t RC_LANES = 16;
+__global__ void __launch_bounds__(256) k_rowcol16(uint32_t* __restrict__ rc, const uint32_t* __restrict__ raw, int c) {
+  KGS_AUX_PRIO();
+  const int l = c / 2, h = c - 1 - l;
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t line = gid / RC_LANES, j = gid % RC_LANES;
+  const uint32_t nlines = (1u << h) + (1u << l);
+  const bool row = line < (1u << h);
+  const uint32_t n = row ? 1u << l : 1u << h;  // elements of this row / column (<= 256)
+  g1_acc29 v;
+  v.set_inf();
+  if (line < nlines) {
+    for (uint32_t t = j; t < n; t += RC_LANES) {
+      const uint32_t b = row ? (line << l) | t : (t << l) | (line - (1u << h));
+      if (b) v.add(g1_acc29::load_raw(run_rec(raw, b)));
+    }
+  }
+#pragma unroll
+  for (int m = RC_LANES / 2; m >= 1; m >>= 1) v.add(shfl_xor_acc(v, m));  // every lane of the wave
+  if (line < nlines && j == 0) v.store_raw(rc + (uint64_t)RAW29_WORDS * line);
+}
+
 // one block per k < c: T_k = sum of the column sums with bit k set (k < l), of the row sums with bit
 // k - l set (l <= k < c-1), or S_B (k = c-1); 256-bit XYZZ out for the host
 __global__ void __launch_bounds__(128) k_bitsum_rc(uint32_t* __restrict__ T, const uint32_t* __restrict__ rc,
@@ -954,7 +980,14 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
                      (uint32_t)L, stride);
   if (ev) hipEventRecord(ev[3], st);
   // row / column sums (2^h + 2^l blocks), then the c bit sums
-  hipLaunchKernelGGL(k_rowcol, dim3((1u << (c - 1 - c / 2)) + (1u << (c / 2))), dim3(256), 0, st, w.part, w.raw29, c);
+  const uint32_t nlines = (1u << (c - 1 - c / 2)) + (1u << (c / 2));
+#ifndef KGS_ROWCOL16
+#define KGS_ROWCOL16 1
+#endif
+  if (exclusive_acc || !KGS_ROWCOL16)
+    hipLaunchKernelGGL(k_rowcol, dim3(nlines), dim3(256), 0, st, w.part, w.raw29, c);
+  else
+    hipLaunchKernelGGL(k_rowcol16, dim3((nlines * RC_LANES + 255) / 256), dim3(256), 0, st, w.part, w.raw29, c);
   hipLaunchKernelGGL(k_bitsum_rc, dim3(c), dim3(128), 0, st, T_out, w.part, w.raw29, c);
   if (ev) hipEventRecord(ev[4], st);
 }
