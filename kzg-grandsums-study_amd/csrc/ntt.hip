@@ -302,10 +302,17 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
                                           uint32_t col, uint32_t jb, uint32_t js, int K, int logd, int lb, int kp0) {
   fr x[1 << R];
   if (GIN && !DIT && io.in && io.pre && R >= 2) {
-    // first DIF pass with a coset pre-scaling: the products two at a time
+    // first DIF pass with a coset pre-scaling: the products two at a time. A pair past the input
+    // (the zero upper half of a degree < n polynomial on a 2n coset: the top j-bit, i.e. r >= 2^(R-1)
+    // for every lane) stays zero without its products
 #pragma unroll
     for (int r = 0; r < (1 << R); r += 2) {
       const uint32_t i0 = lds_idx(col, jb + js * r, K, logd), i1 = lds_idx(col, jb + js * (r + 1), K, logd);
+      if (__builtin_expect(__all(i0 >= io.in_len && i1 >= io.in_len), 0)) {
+        x[r] = fr::zero();
+        x[r + 1] = fr::zero();
+        continue;
+      }
       const fr a0 = i0 < io.in_len ? fr::load(io.in + 8 * i0) : fr::zero();
       const fr a1 = i1 < io.in_len ? fr::load(io.in + 8 * i1) : fr::zero();
       fr::mul_nored_x2(a0, fr::load(io.pre + 8 * i0), a1, fr::load(io.pre + 8 * i1), x[r], x[r + 1]);
