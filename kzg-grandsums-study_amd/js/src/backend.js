@@ -94,9 +94,18 @@ const GC_DELAY_MS = (() => {
     const v = parseInt(process.env.KGS_JS_EAGER_GC || "", 10);
     return Number.isFinite(v) && v > 1 ? v : 5;
 })();
-function scheduleCollect() {
-    if (process.env.KGS_JS_EAGER_GC === "0") return;
-    setTimeout(collectNow, GC_DELAY_MS);
+// Only proofs whose inputs are large enough for their garbage to matter (>= 16 MiB of F / T, e.g.
+// n >= 2^18 for one pair) schedule it, and at most one collection is pending at a time: small proofs
+// take less than the collection itself.
+const GC_MIN_BYTES = 16 << 20;
+let gcPending = false;
+function scheduleCollect(inputBytes) {
+    if (process.env.KGS_JS_EAGER_GC === "0" || gcPending || inputBytes < GC_MIN_BYTES) return;
+    gcPending = true;
+    setTimeout(() => {
+        gcPending = false;
+        collectNow();
+    }, GC_DELAY_MS);
 }
 let gcFn;
 function collectNow() {
@@ -164,7 +173,9 @@ async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT) {
         setLanes(slot);
         const t0 = process.hrtime.bigint();
         const pending = load().prove(slot.ctx, kind, nBits, evalsF, evalsT, selF, selT);
-        if (slot.lanes === 2) scheduleCollect();  // alone on its device: see collectNow
+        if (slot.lanes === 2) {  // alone on its device: see collectNow
+            scheduleCollect(evalsF.concat(evalsT).reduce((a, e) => a + e.length, 0));
+        }
         const res = await pending;
         // diagnostics of the last call: the native call's wall time, its [queue -> worker, worker ->
         // completion] waits, time inside libkgs, kgs_last_timing rounds / copy / prover / write-back

@@ -19,7 +19,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-VALU_PER_PROOF = 5953e6  # wave64 VALU instructions of one 2^20 grand-sum proof (counter pass)
+VALU_PER_PROOF = 5463.5e6  # wave64 VALU instructions of one 2^20 grand-sum proof (round-4 counter pass, profiles/r04/check/valu_share.txt)
 
 
 def main():
