@@ -28,7 +28,6 @@
 #include <functional>
 #include <atomic>
 #include <thread>
-#include <emmintrin.h>
 #include <vector>
 
 #include "../../include/kgs.h"
@@ -1296,33 +1295,6 @@ namespace kgsi {
 // proof once inputs are fed in pieces); the calling thread copies too, so a busy pool never stalls it.
 static std::atomic<int> g_copy_active{0};
 namespace {
-// One piece of a host copy. Into a 16-byte aligned destination (the pinned staging, the caller's
-// output buffers) with non-temporal stores: the destination lines are written whole, so no
-// read-for-ownership of memory that is about to be overwritten (KGS_COPY_NT=0: plain memcpy).
-static void copy_piece(uint8_t* dst, const uint8_t* src, size_t len) {
-  static const bool nt = [] {
-    const char* e = getenv("KGS_COPY_NT");
-    return !(e && e[0] == '0');
-  }();
-  if (!nt || ((uintptr_t)dst & 15) || len < 4096) {
-    memcpy(dst, src, len);
-    return;
-  }
-  size_t i = 0;
-  for (; i + 64 <= len; i += 64) {
-    const __m128i a = _mm_loadu_si128((const __m128i*)(src + i));
-    const __m128i b = _mm_loadu_si128((const __m128i*)(src + i + 16));
-    const __m128i c = _mm_loadu_si128((const __m128i*)(src + i + 32));
-    const __m128i d = _mm_loadu_si128((const __m128i*)(src + i + 48));
-    _mm_stream_si128((__m128i*)(dst + i), a);
-    _mm_stream_si128((__m128i*)(dst + i + 16), b);
-    _mm_stream_si128((__m128i*)(dst + i + 32), c);
-    _mm_stream_si128((__m128i*)(dst + i + 48), d);
-  }
-  if (i < len) memcpy(dst + i, src + i, len - i);
-  _mm_sfence();
-}
-
 struct CopyTask {
   std::vector<CopyJob> pieces;
   std::atomic<size_t> next{0}, done{0};
@@ -1331,7 +1303,7 @@ struct CopyTask {
   void work() {
     size_t i, mine = 0;
     while ((i = next.fetch_add(1)) < pieces.size()) {
-      copy_piece(pieces[i].dst, pieces[i].src, pieces[i].len);
+      memcpy(pieces[i].dst, pieces[i].src, pieces[i].len);
       mine++;
     }
     if (mine && done.fetch_add(mine) + mine == pieces.size()) {
