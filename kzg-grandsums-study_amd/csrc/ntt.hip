@@ -297,7 +297,7 @@ __device__ __forceinline__ void bfly_pair_x2(fr* x, int r0, int r1, int dist, co
 }
 // one register round of R stages of a pass on the 2^R elements j = jb + js * r (r < 2^R) of column
 // col: stage k of the round is pass stage kp0 + k; DIF pairs (r, r + 2^(R-1-k)), DIT (r, r + 2^k)
-template <int R, bool DIT, bool GIN, bool GOUT>
+template <int R, bool DIT, bool GIN, bool GOUT, bool PF>
 __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restrict__ tw, const ntt_io& io, uint32_t cl,
                                           uint32_t col, uint32_t jb, uint32_t js, int K, int logd, int lb, int kp0) {
   fr x[1 << R];
@@ -351,20 +351,32 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
         triv[k * half + qa] = __all(t0 == 0 && t1 == 0);
       }
     }
-    fr wa = fr::load(tw + 8 * tw0[0]), wb = fr::load(tw + 8 * tw1[0]);
+    // PF: the next step's twiddles loaded before this step's butterflies (the 2-wave build); the
+    // 3-wave build (<= 168 VGPRs) loads each step's own twiddles, which saves their registers
+    fr wa, wb;
+    if (PF) {
+      wa = fr::load(tw + 8 * tw0[0]);
+      wb = fr::load(tw + 8 * tw1[0]);
+    }
 #pragma unroll
     for (int st = 0; st < NSTEP; st++) {
       const int k = st / half, qa = st % half;
       const int dist = DIT ? 1 << k : 1 << (R - 1 - k);
       const int r0 = ((qa / dist) * 2 * dist) + (qa % dist), r1 = (((qa + half) / dist) * 2 * dist) + ((qa + half) % dist);
-      const int nx = st + 1 < NSTEP ? st + 1 : st;  // the last step reloads its own twiddles (unused)
-      const fr na = fr::load(tw + 8 * tw0[nx]), nb = fr::load(tw + 8 * tw1[nx]);
-      if (triv[st])
+      if (PF) {
+        const int nx = st + 1 < NSTEP ? st + 1 : st;  // the last step reloads its own twiddles (unused)
+        const fr na = fr::load(tw + 8 * tw0[nx]), nb = fr::load(tw + 8 * tw1[nx]);
+        if (triv[st])
+          bfly_pair_triv(x, r0, r1, dist);
+        else
+          bfly_pair_x2<DIT>(x, r0, r1, dist, wa, wb);
+        wa = na;
+        wb = nb;
+      } else if (triv[st]) {
         bfly_pair_triv(x, r0, r1, dist);
-      else
-        bfly_pair_x2<DIT>(x, r0, r1, dist, wa, wb);
-      wa = na;
-      wb = nb;
+      } else {
+        bfly_pair_x2<DIT>(x, r0, r1, dist, fr::load(tw + 8 * tw0[st]), fr::load(tw + 8 * tw1[st]));
+      }
     }
   } else
 #endif
@@ -418,14 +430,14 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
 // tile (a thread holds the 2^R elements that differ in those bits, the other K - R bits fixed).
 // DIF rounds run from the top j-bits down, DIT rounds from bit 0 up; kp0 = the round's first stage
 // within the pass.
-template <int R, bool DIT, bool GIN, bool GOUT>
+template <int R, bool DIT, bool GIN, bool GOUT, bool PF>
 __device__ __forceinline__ void lds_round_all(uint32_t* lds, const uint32_t* __restrict__ tw, const ntt_io& io,
                                               uint32_t col0, int K, int logd, int lblog, int b0) {
   const int kp0 = DIT ? b0 : K - b0 - R;
   for (uint32_t g = threadIdx.x; g < (LDS_ELEMS >> R); g += LDS_NT) {
     const uint32_t cl = g & ((1u << lblog) - 1), jq = g >> lblog;
     const uint32_t jb = (jq & ((1u << b0) - 1)) | ((jq >> b0) << (b0 + R));
-    lds_round<R, DIT, GIN, GOUT>(lds, tw, io, cl, col0 + cl, jb, 1u << b0, K, logd, 1 << lblog, kp0);
+    lds_round<R, DIT, GIN, GOUT, PF>(lds, tw, io, cl, col0 + cl, jb, 1u << b0, K, logd, 1 << lblog, kp0);
   }
 }
 
@@ -440,6 +452,10 @@ __device__ __forceinline__ void lds_round_all(uint32_t* lds, const uint32_t* __r
 // WV = 2 build in all 5 same-box reps on two boxes (profiles/r04/coresidency/, profiles/r04/ntt/).
 // Contexts proving one proof at a time (two MSM lanes, the latency mode) and every other caller
 // launch WV = 2; in-flight contexts (one lane) WV = 3 (ntt_set_coresident).
+// A/B knob: KGS_NTT_PF3=1 keeps the twiddle prefetch in the 3-wave build too
+#ifndef KGS_NTT_PF3
+#define KGS_NTT_PF3 0
+#endif
 template <int K1, int K2, int K3, bool DIT, bool DIRECT, int WV>
 __global__ void __launch_bounds__(LDS_NT) __attribute__((amdgpu_waves_per_eu(WV, WV)))
 k_ntt_lds_pass(ntt_io io, const uint32_t* __restrict__ tw, int s0) {
@@ -468,14 +484,15 @@ k_ntt_lds_pass(ntt_io io, const uint32_t* __restrict__ tw, int s0) {
     __syncthreads();
   }
   // DIF: bits [K-K1, K), [K-K1-K2, K-K1), [0, K3); DIT: [0, K1), [K1, K1+K2), [K1+K2, K)
-  lds_round_all<K1, DIT, DIRECT, false>(lds, tw, io, col0, K, logd, LBLOG, DIT ? 0 : K - K1);
+  constexpr bool PF = WV < 3 || KGS_NTT_PF3;
+  lds_round_all<K1, DIT, DIRECT, false, PF>(lds, tw, io, col0, K, logd, LBLOG, DIT ? 0 : K - K1);
   __syncthreads();
   if constexpr (K3 > 0) {
-    lds_round_all<K2, DIT, false, false>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 : K3);
+    lds_round_all<K2, DIT, false, false, PF>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 : K3);
     __syncthreads();
-    lds_round_all<K3, DIT, false, DIRECT>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 + K2 : 0);
+    lds_round_all<K3, DIT, false, DIRECT, PF>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 + K2 : 0);
   } else {
-    lds_round_all<K2, DIT, false, DIRECT>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 : 0);
+    lds_round_all<K2, DIT, false, DIRECT, PF>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 : 0);
   }
   if (!DIRECT) {  // store (address order)
     __syncthreads();
