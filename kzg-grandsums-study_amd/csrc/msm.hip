@@ -100,10 +100,14 @@ void msm_build_table(hipStream_t st, uint32_t* table, uint64_t npts, int c, int 
 //  pass 2 sorts every partition by lo = key - (p << LOB) inside one workgroup, tile by tile
 //          through LDS (again run-wise stores), and writes the bucket offsets.
 // Order inside a bucket is unspecified (point addition is commutative).
-template <int C>
-__device__ __forceinline__ void scalar_digits(int32_t (&d)[(255 + C - 1) / C], const uint32_t* sc, uint64_t i) {
+// digits of scalar i: from the Montgomery-form scalars (STD = false) or from their standard forms
+// (STD = true: k_sort_hist stores them for k_sort_part, which then skips the conversion)
+template <int C, bool STD = false>
+__device__ __forceinline__ void scalar_digits(int32_t (&d)[(255 + C - 1) / C], const uint32_t* sc, uint64_t i,
+                                              uint32_t* std_out = nullptr) {
   constexpr int W = (255 + C - 1) / C;
-  fr s = fr::load(sc + 8 * i).from_mont();
+  fr s = STD ? fr::load(sc + 8 * i) : fr::load(sc + 8 * i).from_mont();
+  if (std_out) s.store(std_out + 8 * i);
   constexpr int32_t half = 1 << (C - 1);
   constexpr uint32_t mask = (1u << C) - 1;
   uint32_t carry = 0;
@@ -155,7 +159,8 @@ constexpr int SORT_SPT = KGS_SORT_SPT;  // scalars per thread in the histogram /
 
 template <int C>
 __global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ bh, const uint32_t* __restrict__ sc,
-                                                   uint64_t N, int lob, int NH, uint32_t nblk) {
+                                                   uint64_t N, int lob, int NH, uint32_t nblk,
+                                                   uint32_t* __restrict__ std_out) {
   KGS_AUX_PRIO();
   // per-block partition histogram, stored transposed: bh[p * nblk + block]
   constexpr int W = (255 + C - 1) / C;
@@ -166,7 +171,7 @@ __global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ bh, co
     const uint64_t i = ((uint64_t)blockIdx.x * SORT_SPT + q) * 256 + threadIdx.x;
     if (i < N) {
       int32_t d[W];
-      scalar_digits<C>(d, sc, i);
+      scalar_digits<C>(d, sc, i, std_out);
 #pragma unroll
       for (int j = 0; j < W; j++) {
         if (d[j]) atomicAdd(&h[part_of((uint32_t)(d[j] < 0 ? -d[j] : d[j]), lob)], 1u);
@@ -259,7 +264,7 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
     const uint64_t i = ((uint64_t)blk * SORT_SPT + q) * 256 + tid;
     if (i < N) {
       int32_t d[W];
-      scalar_digits<C>(d, sc, i);
+      scalar_digits<C, true>(d, sc, i);  // sc: the standard forms k_sort_hist stored
 #pragma unroll
       for (int j = 0; j < W; j++) {
         if (!d[j]) continue;
@@ -921,14 +926,17 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   uint32_t* cpre = w.cursor + 300;     // NH + 1: lo-pass chunks per partition, exclusive scan
   uint32_t* bh = w.blockhist;          // NH x nblk
   const size_t part_lds = (size_t)256 * SORT_SPT * W * 6;
+  // the scalars' standard forms (32 B each) go through w.sorted between the two sort passes: only the
+  // lo pass writes it later, and it holds E = N * W >= 8 N words (W >= 9 for c <= 31)
+  uint32_t* scal_std = w.sorted;
   switch (c) {
 #define KGS_SORT_C(CC)                                                                                         \
   case CC:                                                                                                      \
-    hipLaunchKernelGGL(k_sort_hist<CC>, dim3(nblk), dim3(256), 0, st, bh, scalars, N, lob, NH, nblk);         \
+    hipLaunchKernelGGL(k_sort_hist<CC>, dim3(nblk), dim3(256), 0, st, bh, scalars, N, lob, NH, nblk, scal_std); \
     hipLaunchKernelGGL(k_sort_scan_blocks, dim3(NH), dim3(256), 0, st, bh, ptot, nblk);                       \
     hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(64), 0, st, hi_off, ptot, NH, w.offsets, B, cpre);         \
     hipLaunchKernelGGL(k_sort_part<CC>, dim3(nblk), dim3(256), part_lds, st, (uint32_t*)w.digit, w.lo, bh,   \
-                       ptot, hi_off, scalars, N, tb.npts, pbase, pstride, lob, NH, nblk);                     \
+                       ptot, hi_off, scal_std, N, tb.npts, pbase, pstride, lob, NH, nblk);                    \
     break;
     KGS_SORT_C(7) KGS_SORT_C(8) KGS_SORT_C(9) KGS_SORT_C(10) KGS_SORT_C(11) KGS_SORT_C(12)
     KGS_SORT_C(13) KGS_SORT_C(14) KGS_SORT_C(15) KGS_SORT_C(16) KGS_SORT_C(17)
