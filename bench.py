@@ -20,8 +20,14 @@ script launches its own N ranks (torch.distributed.run, 127.0.0.1) as a child pr
 
 Extra fields in the JSON line:
   proof_verified : one proof of the timed workload checked with the native verifier (pairing)
-  host_buffer_boundary : PCIe-inclusive latency of kgs_prove on pageable host buffers (the drop-in path)
-  latency_ms_single_proof / round_ms_single_proof : one proof at a time on one context (2 MSM lanes)
+  host_buffer_inflight : the same steps, in flight the same way, through the drop-in boundary: kgs_prove
+              on pageable host F/T with the Montgomery write-back into caller-owned host buffers
+              (prover.js:147-148) — PCIe-inclusive, so never `value`; `vs_device_resident` is its ratio
+              to `value`, and the host path's proof must equal the device path's
+  host_buffer_boundary : single-proof latency of kgs_prove on pageable host buffers (median / spread of
+              7) and of the JavaScript drop-in module (javascript_module: median / spread of its samples)
+  latency_ms_single_proof / latency_single_proof_ms / round_ms_single_proof : one proof at a time on one
+              context (2 MSM lanes), device-resident inputs, median and spread of 7
   msm       : live HIP-event timing of the MSM phases at N = n (points/s, G1 adds/s)
   roofline  : the dominant kernel (MSM bucket accumulation, k_accumulate) in algorithmic Fq products/s
               against the chip's mad-only product rate (INT-VALU bound); traffic =
@@ -338,11 +344,14 @@ def main():
     t_load = time.time() - t0
     power, npts, window_c = ctx.srs_info()
 
-    # inputs resident in HBM (one set per in-flight context)
+    # inputs per in-flight context: pageable host buffers (the drop-in boundary, kgs_prove) and a
+    # device-resident copy of the same multiset (kgs_prove_device); each context also owns the two
+    # host buffers its Montgomery write-back lands in (prover.js:147-148), recycled across proofs as
+    # the JS module's pool recycles its output buffers
     ctxs = [ctx] + extra
-    bufs, keep = [], []
+    bufs, hbufs, keep = [], [], []
     for ci, _ in enumerate(ctxs):
-        d_f, d_t = [], []
+        d_f, d_t, h_f, h_t = [], [], [], []
         for i in range(args.npols):
             f, t = synth_evals(n, 1000 * rank + 100 * ci + i)
             tf = torch.from_numpy(f.reshape(-1).copy()).to(f"cuda:{local}")
@@ -350,97 +359,134 @@ def main():
             keep += [tf, tt]
             d_f.append(tf.data_ptr())
             d_t.append(tt.data_ptr())
+            h_f.append(f.tobytes())
+            h_t.append(t.tobytes())
+        wb = ([bytearray(32 * n) for _ in range(args.npols)], [bytearray(32 * n) for _ in range(args.npols)])
         bufs.append((d_f, d_t))
+        hbufs.append((h_f, h_t, wb))
     torch.cuda.synchronize()
 
-    def run(ci, count):
+    def run_dev(ci, count):
         c = ctxs[ci]
         d_f, d_t = bufs[ci]
         for _ in range(count):
             c.prove_device(kind, nbits, d_f, d_t)
 
-    def steps(total):
+    def run_host(ci, count):
+        c = ctxs[ci]
+        h_f, h_t, wb = hbufs[ci]
+        for _ in range(count):
+            c.prove(kind, nbits, h_f, h_t, mont_out=wb)
+
+    def steps(total, fn=run_dev):
         if len(ctxs) == 1:
-            run(0, total)
+            fn(0, total)
             return
-        import threading
         share = [total // len(ctxs) + (1 if i < total % len(ctxs) else 0) for i in range(len(ctxs))]
-        th = [threading.Thread(target=run, args=(i, share[i])) for i in range(len(ctxs))]
+        th = [threading.Thread(target=fn, args=(i, share[i])) for i in range(len(ctxs))]
         for x in th:
             x.start()
         for x in th:
             x.join()
+
+    def stats_ms(xs):
+        xs = sorted(1000.0 * x for x in xs)
+        return {"median": round(float(np.median(xs)), 3), "min": round(xs[0], 3), "max": round(xs[-1], 3),
+                "samples": len(xs)}
 
     # throughput contexts: one MSM lane each (the in-flight proofs keep the GPU busy); the
     # single-proof latency below uses context 0 with two lanes (kgs_ctx_set_msm_lanes)
     for c in ctxs:
         c.set_msm_lanes(1 if len(ctxs) > 1 else 2)
     log("warm-up")
-    steps(max(args.warmup, len(ctxs)))
-    # single-proof latency (one proof at a time on one context), outside the timed region
+    steps(max(args.warmup, len(ctxs)), run_dev)
+    steps(max(args.warmup, len(ctxs)), run_host)
+    # single-proof latency (one proof at a time on one context), outside the timed region: median and
+    # spread of LAT_SAMPLES proofs, device-resident and through the host-buffer boundary
+    LAT_SAMPLES = 7
     ctx.set_msm_lanes(2)
-    run(0, 1)
+    run_dev(0, 1)
     t_lat = []
-    for _ in range(3):
+    for _ in range(LAT_SAMPLES):
         t1 = time.perf_counter()
-        run(0, 1)
+        run_dev(0, 1)
         t_lat.append(time.perf_counter() - t1)
-    latency_ms = 1000.0 * min(t_lat)
     rounds = ctx.last_timing()
-    # the proofs the bench times are real: check one with the native verifier (pairing)
+    run_host(0, 1)
+    t_hlat, h_timing = [], []
+    for _ in range(LAT_SAMPLES):
+        t1 = time.perf_counter()
+        run_host(0, 1)
+        t_hlat.append(time.perf_counter() - t1)
+        h_timing.append(ctx.last_timing())
+    latency = stats_ms(t_lat)
+    latency_ms = latency["median"]
+    # the proofs the bench times are real: one device-resident proof checked with the native verifier
+    # (pairing), and the host-buffer path must give the identical proof and write back F's Montgomery form
     d_f0, d_t0 = bufs[0]
     coms0, evs0 = ctx.prove_device(kind, nbits, d_f0, d_t0)
     cn0, en0 = K.proof_names(kind, args.npols, False)
     vf = K.grandsum_verifier if kind == K.GRANDSUM else K.grandproduct_verifier
     proof_verified = vf(ptau, {"commitments": dict(zip(cn0, coms0)), "evaluations": dict(zip(en0, evs0))}, nbits)
+    h_f0, h_t0, _ = hbufs[0]
+    hcoms, hevs, hmf, _ = ctx.prove(kind, nbits, h_f0, h_t0)
+    host_identical = hcoms == coms0 and hevs == evs0 and bytes(hmf[0][:32 * 64]) == ctx.fr_to_mont(h_f0[0][:32 * 64])
     ctx.set_msm_lanes(1 if len(ctxs) > 1 else 2)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    log("timed region")
-    with roctx_range("kgs_bench_timed_region"):
-        ts = time.perf_counter()
-        steps(args.steps)
-        torch.cuda.synchronize()
+
+    def timed(fn, label):
         if dist:
             dist.barrier()
-        elapsed = time.perf_counter() - ts
-    elapsed = max_over_ranks(elapsed)
+        torch.cuda.synchronize()
+        with roctx_range(label):
+            ts = time.perf_counter()
+            steps(args.steps, fn)
+            torch.cuda.synchronize()
+            if dist:
+                dist.barrier()
+            return max_over_ranks(time.perf_counter() - ts)
+
+    # headline: device-resident inputs (the contract's `value`: inputs in HBM when the timed region
+    # starts); right after it the same proofs through the host-buffer boundary, in flight the same way
+    log("timed region")
+    elapsed = timed(run_dev, "kgs_bench_timed_region")
     total_proofs = args.steps * world
     value = total_proofs / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
+    log(f"timed: {value:.2f} proofs/s device-resident; host-buffer in flight")
+    el_host = timed(run_host, "kgs_bench_host_region")
+    host_inflight = {
+        "proofs_per_s": round(total_proofs / el_host, 4), "ms_per_step": round(1000.0 * el_host / args.steps, 3),
+        "vs_device_resident": round(el_host and (total_proofs / el_host) / value, 4),
+        "proof_identical_to_device_path": host_identical,
+        "note": (f"kgs_prove on pageable host F/T, {len(ctxs)} contexts in flight, Montgomery forms written back into "
+                 "caller-owned host buffers (prover.js:147-148): PCIe-inclusive, same steps as `value`")}
 
-    # ---------------- host-buffer boundary (what the JS / Python drop-in modules call): kgs_prove on
-    # pageable host buffers, including the H2D copy of F/T and the D2H Montgomery write-back
-    log(f"timed: {value:.2f} proofs/s; host-buffer and JS legs")
+    # ---------------- host-buffer boundary latency (what the JS / Python drop-in modules call): kgs_prove
+    # on pageable host buffers, including the H2D copy of F/T and the D2H Montgomery write-back
+    log(f"host-buffer in flight: {host_inflight['proofs_per_s']:.2f} proofs/s; JS leg")
     host_leg = None
     if rank == 0 and args.host_leg:
-        hf = [synth_evals(n, 1000 * rank + i)[0].tobytes() for i in range(args.npols)]
-        ht = [synth_evals(n, 1000 * rank + i)[1].tobytes() for i in range(args.npols)]
-        ctx.set_msm_lanes(2)  # one proof at a time: the single-proof latency mode, as latency_ms_single_proof
-        ctx.prove(kind, nbits, hf, ht)  # warm
-        t_host = []
-        for _ in range(3):
-            t1 = time.perf_counter()
-            ctx.prove(kind, nbits, hf, ht)
-            t_host.append(time.perf_counter() - t1)
-        ctx.set_msm_lanes(1 if len(ctxs) > 1 else 2)
-        el = sum(t_host) / len(t_host)
-        host_leg = {"ms_per_proof": round(1000.0 * el, 3), "proofs_per_s": round(1.0 / el, 3),
-                    "ms_best": round(1000.0 * min(t_host), 3),
-                    "note": "single context (2 MSM lanes), one proof at a time, mean of 3; F/T in pageable host memory, Montgomery forms written back (prover.js:147-148)"}
+        hl = stats_ms(t_hlat)
+        best = min(range(len(t_hlat)), key=lambda i: t_hlat[i])
+        host_leg = {"ms_per_proof": hl["median"], "latency_ms": hl, "proofs_per_s": round(1000.0 / hl["median"], 3),
+                    "ms_best": hl["min"], "libkgs_timing_ms_best": [round(x, 3) for x in h_timing[best]],
+                    "note": f"single context (2 MSM lanes), one proof at a time, median of {LAT_SAMPLES}; F/T in "
+                            "pageable host memory, Montgomery forms written back (prover.js:147-148)"}
 
         # the JavaScript drop-in module itself (north star: JS host -> N-API -> libkgs), if node and
-        # the addon are present: best of 5 proofs, fresh inputs each, last proof verified
+        # the addon are present: 7 proofs, fresh inputs each, last proof verified
         import shutil
         import subprocess
         js_dir = os.path.join(HERE, "kzg-grandsums-study_amd", "js")
         if shutil.which("node") and os.path.exists(os.path.join(js_dir, "build", "kgs_addon.node")):
             try:
-                # latency: best of 5 one-at-a-time proofs; throughput: 16 concurrent chains of 5
+                # latency: 7 one-at-a-time proofs (best, median, spread; the library default, and a
+                # caller that runs gc() between its calls); throughput: 16 concurrent chains of 7
                 # awaited prover() calls over the module's context pool (8 contexts on this GPU)
                 env = dict(os.environ, KGS_JS_CONTEXTS=str(2 * args.inflight), KGS_DEVICES=str(local))
-                out = subprocess.run(["node", os.path.join(js_dir, "test", "time_prove.js"), ptau, str(nbits), "5",
+                env.pop("KGS_JS_EAGER_GC", None)
+                out = subprocess.run(["node", "--expose-gc", os.path.join(js_dir, "test", "time_prove.js"), ptau,
+                                      str(nbits), "7",
                                       str(4 * args.inflight)], capture_output=True, text=True, timeout=300, env=env)
                 host_leg["javascript_module"] = json.loads(out.stdout.strip().splitlines()[-1])
             except Exception as e:  # the JS leg must not hide the GPU number
@@ -571,8 +617,10 @@ def main():
                    "srs_power": power, "srs_points_resident": npts, "srs_gen_s": round(t_gen, 2),
                    "srs_load_s": round(t_load, 2)},
         "proof_verified": proof_verified,
+        "host_buffer_inflight": host_inflight,
         "host_buffer_boundary": host_leg,
         "latency_ms_single_proof": round(latency_ms, 3),
+        "latency_single_proof_ms": latency,
         "round_ms_single_proof": [round(x, 3) for x in rounds],
         "msm": msm,
         "roofline": roofline,

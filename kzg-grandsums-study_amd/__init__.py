@@ -482,11 +482,19 @@ class Context:
     # ---- full prover ----
     def prove(self, kind, nbits, evals_f, evals_t, sel_f=None, sel_t=None, mont_out=True):
         """Host-buffer prover; returns (commitment list, evaluation list, mont_f, mont_t). Inputs
-        are read in place; the Montgomery forms come back as bytearrays (no extra copies)."""
+        are read in place; the Montgomery forms come back as bytearrays (no extra copies).
+        mont_out: True (new bytearrays), False (no write-back), or a pair of lists (mont_f, mont_t)
+        of writable caller buffers of 32 * 2^nbits bytes each that receive the Montgomery forms (a
+        caller that recycles its output buffers, as the JS module's pool does)."""
         k = len(evals_f)
         n = 1 << nbits
         if any(len(x) != 32 * n for x in list(evals_f) + list(evals_t)):
             raise ValueError("evaluation buffers must hold 2^nbits 32-byte elements")
+        given = None
+        if isinstance(mont_out, (tuple, list)):
+            given = (list(mont_out[0]), list(mont_out[1]))
+            if len(given[0]) != k or len(given[1]) != k or any(len(x) != 32 * n for x in given[0] + given[1]):
+                raise ValueError("write-back buffers must be two lists of npols buffers of 2^nbits 32-byte elements")
         keep = []
         PF = (ctypes.c_void_p * k)()
         PT = (ctypes.c_void_p * k)()
@@ -498,7 +506,7 @@ class Context:
             keep += [kf, kt]
             PF[i], PT[i] = pf, pt
             if mont_out:
-                ma, mb = _uninit_bytearray(32 * n), _uninit_bytearray(32 * n)
+                ma, mb = (given[0][i], given[1][i]) if given else (_uninit_bytearray(32 * n), _uninit_bytearray(32 * n))
                 (pa, ka), (pb, kb) = _ptr(ma), _ptr(mb)
                 keep += [ka, kb]
                 mf.append(ma)

@@ -98,7 +98,11 @@ void ensure_domain(kgs_ctx& c, int logM) {
   d->coset_pow = d->tw_inv + 8 * M;
   d->coset_ipow = d->coset_pow + 8 * M;
   d->invm = d->coset_ipow + 8 * M;
-  c.reset_staging();
+  // This may run in the middle of a proof (the reference-quirks replay grows the domain,
+  // ref_quirks.cpp need_domain): the scalars and pinned words the proof has staged so far must stay
+  // intact, so the build stages above them and gives that space back once it has completed.
+  c.sync();
+  const size_t pin_mark = c.h_pin_off, scal_mark = c.d_scal_off;
   std::vector<Fr> consts;
   for (int l = 0; l < logM; l++) {
     Fr w = fr_w(l + 1);
@@ -122,7 +126,9 @@ void ensure_domain(kgs_ctx& c, int logM) {
   for (int l = 0; l <= logM; l++) im[l].to_bytes(h + 32 * l);
   HC(hipMemcpyAsync(d->invm, h, 32 * (logM + 1), hipMemcpyHostToDevice, c.st));
   check_launch();
-  c.reset_staging();  // built: publish
+  c.sync();  // built: publish
+  c.h_pin_off = pin_mark;
+  c.d_scal_off = scal_mark;
   d->logM = logM;
   g_dom_reg.erase(std::remove_if(g_dom_reg.begin(), g_dom_reg.end(), [](auto& w) { return w.expired(); }),
                   g_dom_reg.end());

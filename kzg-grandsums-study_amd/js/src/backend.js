@@ -80,47 +80,38 @@ async function withContext(fn) {
     }
 }
 
-// Eager collection beside a lone proof. Every proof leaves the caller's previous input buffers (the
-// reference replaces Evaluations.eval by the Montgomery copy, prover.js:147-148) as 64 MiB of garbage
-// at n = 2^20; V8 then finalises a ~6 ms mark-sweep as a main-thread task, which, scheduled while the
-// GPU works, tended to run just as the proof completed: the Promise resolved 0.1-5 ms after the
-// result was ready (profiles/r04/js/). A proof alone on its device therefore runs one full collection
-// right after it is queued, beside its ~15 ms of GPU work; with other proofs in flight V8's own
-// schedule is kept. The collection is started GC_DELAY_MS after the proof is queued: freeing the
-// garbage's pages while round 1 copies the next inputs into pinned staging stretched that round from
-// 3.4 to 9-15 ms in a third of the samples (profiles/r04/js/run5). KGS_JS_EAGER_GC=0 turns it off,
-// KGS_JS_EAGER_GC=<ms> sets the delay.
+// Eager collection beside a lone proof: OPT-IN (KGS_JS_EAGER_GC=1, or =<ms> for the delay), and only
+// in an application that itself started Node with --expose-gc (the library never changes V8 flags).
+// Why it exists: every proof leaves the caller's previous input buffers (the reference replaces
+// Evaluations.eval by the Montgomery copy, prover.js:147-148) as 64 MiB of garbage at n = 2^20; V8
+// then finalises a ~6 ms mark-sweep as a main-thread task, which, scheduled while the GPU works, tended
+// to run just as the proof completed: the Promise resolved 0.1-5 ms after the result was ready
+// (profiles/r04/js/). With the opt-in, a proof alone on its device runs one full collection
+// GC_DELAY_MS after it is queued, beside its ~15 ms of GPU work (not at once: freeing the garbage's
+// pages while round 1 copies the next inputs into pinned staging stretched that round from 3.4 to
+// 9-15 ms in a third of the samples, profiles/r04/js/run5); with other proofs in flight V8's own
+// schedule is kept. A blocking full collection on the host application's main thread is its call to
+// make, which is why this is off by default.
 const GC_DELAY_MS = (() => {
     const v = parseInt(process.env.KGS_JS_EAGER_GC || "", 10);
     return Number.isFinite(v) && v > 1 ? v : 5;
 })();
+function eagerGcEnabled() {
+    const v = process.env.KGS_JS_EAGER_GC;
+    return v !== undefined && v !== "" && v !== "0" && typeof global.gc === "function";
+}
 // Only proofs whose inputs are large enough for their garbage to matter (>= 16 MiB of F / T, e.g.
 // n >= 2^18 for one pair) schedule it, and at most one collection is pending at a time: small proofs
 // take less than the collection itself.
 const GC_MIN_BYTES = 16 << 20;
 let gcPending = false;
 function scheduleCollect(inputBytes) {
-    if (process.env.KGS_JS_EAGER_GC === "0" || gcPending || inputBytes < GC_MIN_BYTES) return;
+    if (!eagerGcEnabled() || gcPending || inputBytes < GC_MIN_BYTES) return;
     gcPending = true;
     setTimeout(() => {
         gcPending = false;
-        collectNow();
+        global.gc();
     }, GC_DELAY_MS);
-}
-let gcFn;
-function collectNow() {
-    if (gcFn === undefined) {
-        gcFn = null;
-        if (process.env.KGS_JS_EAGER_GC !== "0") {
-            try {
-                require("v8").setFlagsFromString("--expose_gc");
-                gcFn = require("vm").runInNewContext("gc");
-            } catch (e) {
-                gcFn = null;
-            }
-        }
-    }
-    if (gcFn) gcFn();
 }
 
 // MSM lanes of a proof about to start: two (single-proof latency mode, kgs_ctx_set_msm_lanes) when it
@@ -173,7 +164,7 @@ async function prove(kind, pTauFilename, nBits, evalsF, evalsT, selF, selT) {
         setLanes(slot);
         const t0 = process.hrtime.bigint();
         const pending = load().prove(slot.ctx, kind, nBits, evalsF, evalsT, selF, selT);
-        if (slot.lanes === 2) {  // alone on its device: see collectNow
+        if (slot.lanes === 2) {  // alone on its device: see scheduleCollect (opt-in)
             scheduleCollect(evalsF.concat(evalsT).reduce((a, e) => a + e.length, 0));
         }
         const res = await pending;

@@ -1,9 +1,10 @@
 // Evaluation-form vector: the prover's input container. Same surface as the reference's
 // src/polynomial/evaluations.js:5-136 (fromArray, fromEvals, getOneEvals, getZeroEvals,
 // getRandomEvals, getRandomBinEvals, getEvaluation, getEvaluationSequence, setEvaluation, length,
-// isEqual, isAllZeros, isAllOnes), and fromPolynomial through the curve shim's GPU Fr.fft. The
-// prover itself does not use fromPolynomial: its NTTs run inside libkgs.
+// isEqual, isAllZeros, isAllOnes, print), and fromPolynomial through the curve shim's GPU Fr.fft.
+// The prover itself does not use fromPolynomial: its NTTs run inside libkgs.
 const { BigBuffer } = require("../bigbuffer");
+const logger = require("../logger");
 
 class Evaluations {
     constructor(evaluations, curve) {
@@ -63,6 +64,7 @@ class Evaluations {
     length() {
         const length = this.eval.byteLength / this.Fr.n8;
         if (length !== Math.floor(length)) throw new Error("Polynomial evaluations buffer has incorrect size");
+        if (length === 0) logger.warn("Polynomial has length zero");  // evaluations.js:104-106
         return length;
     }
     isEqual(other) {
@@ -73,12 +75,17 @@ class Evaluations {
     // one element (one native compare, no second vector)
     isConstant(value) {
         const n8 = this.Fr.n8, b = view(this.eval);
-        if (b.length === 0) return true;
+        if (this.length() === 0) return true;  // (the reference's warning, through length())
         if (Buffer.compare(b.subarray(0, n8), view(value)) !== 0) return false;
         return Buffer.compare(b.subarray(n8), b.subarray(0, b.length - n8)) === 0;
     }
     isAllZeros() { return this.isConstant(this.Fr.zero); }
     isAllOnes() { return this.isConstant(this.Fr.one); }
+    // evaluations.js:131-135: one stdout line per element, "<name>(𝛚^i) = <decimal value>"
+    print(name = "f") {
+        for (let i = 0; i < this.length(); i++)
+            console.log(`${name}(𝛚^${i}) =`, this.Fr.toString(this.getEvaluation(i)));
+    }
 }
 
 // Buffer over a Uint8Array's memory (no copy, unlike Buffer.from(typedArray))

@@ -3,7 +3,9 @@
 // Inputs are random standard-form field elements (< 2^253 < r) in Uint8Arrays, T = F rotated by one
 // element, prepared before the timed regions (the prover overwrites them with Montgomery form, so
 // every proof gets its own copy).
-//  * latency: one proof at a time, back to back (inputs prepared beforehand), best of PROOFS;
+//  * latency: one proof at a time, back to back (inputs prepared beforehand): best, median and spread
+//    of PROOFS; under node --expose-gc also a second series in which the caller runs gc() before each
+//    timed call (latency_ms_caller_gc_between);
 //  * concurrent throughput: PROOFS * CONCURRENCY proofs issued as CONCURRENCY independent chains of
 //    awaited prover() calls (the reference API is async; independent calls run on the backend's
 //    context pool), wall clock of the whole batch.
@@ -44,9 +46,29 @@ const { poolInfo, diag } = require("../src/backend");
             bestDiag = { exec_ms: +diag.execMs.toFixed(3), libkgs_timing_ms: diag.timing.map(x => +x.toFixed(3)) };
         }
     }
+    const stats = xs => {
+        const s = xs.slice().sort((a, b) => a - b), m = s.length >> 1;
+        return { median: +(s.length % 2 ? s[m] : (s[m - 1] + s[m]) / 2).toFixed(3), min: s[0], max: s[s.length - 1],
+                 samples: s.length };
+    };
     const verified = await mset_eq_kzg_grandsum_verifier(ptau, proof, nBits);
     const out = { nbits: nBits, proofs, ms_per_proof: +best.toFixed(3), proofs_per_s: +(1000 / best).toFixed(3), verified,
-                  best_inside_libkgs: bestDiag };
+                  latency_ms: stats(all), best_inside_libkgs: bestDiag,
+                  eager_gc: process.env.KGS_JS_EAGER_GC || null };
+    // a caller that collects its own garbage between proofs (node --expose-gc; gc() outside the timed
+    // call): the previous proof's replaced input buffers are freed before the next call starts
+    if (typeof global.gc === "function" && !process.env.KGS_JS_EAGER_GC) {
+        const lat2 = Array.from({ length: proofs }, mk), all2 = [];
+        for (let i = 0; i < proofs; i++) {
+            [F, T] = lat2[i];
+            lat2[i] = null;
+            global.gc();
+            const t0 = process.hrtime.bigint();
+            proof = await mset_eq_kzg_grandsum_prover(ptau, F, T);
+            all2.push(+(Number(process.hrtime.bigint() - t0) / 1e6).toFixed(3));
+        }
+        out.latency_ms_caller_gc_between = stats(all2);
+    }
     if (process.env.KGS_JS_TIME_ALL) {  // every latency sample: [exec_ms, libkgs timing...] each
         out.all_ms = all;
         out.all_inside_libkgs = diags;

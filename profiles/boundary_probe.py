@@ -35,9 +35,11 @@ def main():
     # the same vectors in buffers the caller pinned once (kgs_host_register): DMA'd in place
     rf, rt = [bytearray(f.tobytes())], [bytearray(t.tobytes())]
     handles = [K.host_register(b) for b in rf + rt]
+    wb = ([bytearray(len(hf[0]))], [bytearray(len(ht[0]))])  # recycled caller-owned write-back buffers
     fmt = lambda xs: " ".join(f"{x:6.2f}" for x in xs)  # noqa: E731
     for label, fn in (("device", lambda: ctx.prove_device(K.GRANDSUM, nbits, [df.data_ptr()], [dt.data_ptr()])),
                       ("host", lambda: ctx.prove(K.GRANDSUM, nbits, hf, ht)),
+                      ("host_recycled", lambda: ctx.prove(K.GRANDSUM, nbits, hf, ht, mont_out=wb)),
                       ("host_no_mont", lambda: ctx.prove(K.GRANDSUM, nbits, hf, ht, mont_out=False)),
                       ("host_prereg", lambda: ctx.prove(K.GRANDSUM, nbits, rf, rt, mont_out=False))):
         for _ in range(reps):

@@ -36,3 +36,5 @@ def test_bench_small_run_ok():
     assert line["proof_verified"] is True
     assert line["extra_configs"]["selected_vector"]["proof_verified"] is True
     assert line["roofline"]["achieved"] > 0
+    assert line["host_buffer_inflight"]["proof_identical_to_device_path"] is True
+    assert line["latency_single_proof_ms"]["samples"] >= 5

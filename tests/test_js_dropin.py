@@ -275,6 +275,32 @@ process.stdout.write(JSON.stringify(out));
     assert o["rprbe"] == [1, 2, 3, 4]
 
 
+def test_evaluations_print_and_zero_length_warning():
+    """Evaluations.print(name) writes one stdout line per element, "<name>(𝛚^i) = <decimal>"
+    (/root/reference/src/polynomial/evaluations.js:131-135), and length() of an empty buffer warns
+    "Polynomial has length zero" through the module logger (:104-106). Host only."""
+    script = """
+const { getCurveFromName } = require('./src/curve.js');
+const { Evaluations } = require('./index.js');
+getCurveFromName('bn128').then(c => {
+  const e = Evaluations.fromArray([c.Fr.e(7n), c.Fr.e(-1n), c.Fr.zero], c);
+  e.print('F');
+  e.print();
+  const z = new Evaluations(new Uint8Array(0), c);
+  console.log('len', z.length(), z.isAllZeros());
+});
+"""
+    r = subprocess.run([NODE, "-e", script], cwd=JS, capture_output=True, timeout=60,
+                       env=dict(os.environ, KGS_LOG_LEVEL="WARN"))
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.decode().splitlines()
+    assert lines[:6] == ["F(𝛚^0) = 7", f"F(𝛚^1) = {bn.R - 1}", "F(𝛚^2) = 0",
+                         "f(𝛚^0) = 7", f"f(𝛚^1) = {bn.R - 1}", "f(𝛚^2) = 0"]
+    assert lines[6] == "len 0 true"
+    warns = [x for x in r.stderr.decode().splitlines() if "Polynomial has length zero" in x]
+    assert len(warns) >= 2 and all(x.startswith("[WARN]") for x in warns)
+
+
 @pytest.mark.gpu
 def test_curve_shim_fr_batch_members_on_gpu(tmp_path):
     """Fr.fft / ifft / batchInverse / batchToMontgomery / batchFromMontgomery of the shim
