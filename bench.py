@@ -165,7 +165,8 @@ def make_group(K, torch, dist, rank, world, local):
     """Rank group of the distributed prover for N > 1: RCCL (the communicator id made on rank 0 and
     broadcast through torch.distributed); the gloo rehearsal uses a host all-gather group."""
     if BACKEND == "gloo":
-        return K.Group.host(world, K.torch_allgather()), "host all-gather group (gloo rehearsal)"
+        return (K.Group.host(world, K.torch_allgather(), K.torch_alltoall()),
+                "host all-gather + all-to-all group (gloo rehearsal)")
     uid = K.rccl_unique_id() if rank == 0 else bytes(128)
     t = torch.tensor(list(uid), dtype=torch.uint8, device=coll_device())
     dist.broadcast(t, 0)
@@ -238,6 +239,20 @@ def large_leg(K, torch, dist, rank, world, local, nb, k, selected, proofs, label
         hs = [torch.empty_like(h) for _ in range(world)]
         dist.all_gather(hs, h)
         out["ranks_agree"] = all(bool(torch.equal(hs[0], x)) for x in hs)
+    if world > 1 and group is not None:
+        # the last proof's exchanges (kgs_last_exchange: all-to-all spans by HIP events on the prover's
+        # stream, host all-gathers by the wall clock), max over ranks, against DESIGN.md §6's model
+        x = ctx.last_exchange()
+        ex_ms = max_over_ranks(x["alltoall_ms"] + x["allgather_ms"])
+        model = K.dist_exchange_model(K.GRANDSUM, nb, k, selected, world)
+        out["exchange"] = {
+            "compute_ms": round(1000.0 * el / proofs - ex_ms, 3), "exchange_ms": round(ex_ms, 3),
+            "exchange_bytes": x["alltoall_bytes"] + x["allgather_bytes"],
+            "alltoall": {"n": x["alltoall_n"], "ms_rank0": round(x["alltoall_ms"], 3), "bytes": x["alltoall_bytes"]},
+            "allgather": {"n": x["allgather_n"], "ms_rank0": round(x["allgather_ms"], 3), "bytes": x["allgather_bytes"]},
+            "model_alltoall": model,
+            "note": "per rank, last proof: exchange_ms = max over ranks of the all-to-all spans (transfer + waiting for "
+                    "peers) + host all-gather wall time; compute_ms = ms_per_proof - exchange_ms; bytes leave the rank"}
     ctx.set_shard(0, 1)
     ctx.set_group(None)
     ctx.close()

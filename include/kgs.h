@@ -118,6 +118,12 @@ int kgs_msm_combine(const uint8_t* T_all, int nparts, int c, uint8_t out_lem[64]
 typedef struct kgs_group kgs_group_t;
 int kgs_group_create_local(int world, kgs_group_t** out);
 int kgs_group_create_host(int world, kgs_allgather_fn fn, void* user, kgs_group_t** out);
+/* host transport with a real all-to-all: `a2a(user, send, recv, chunk)` sends chunk j of send (world
+ * chunks of `chunk` bytes) to rank j and receives rank j's chunk for this rank into chunk j of recv
+ * (e.g. torch.distributed all_to_all_single over gloo); returns 0. (W - 1) / W of a vector leaves a
+ * rank per all-to-all, against W x the vector received through the all-gather-only transport. */
+typedef int (*kgs_alltoall_fn)(void* user, const uint8_t* send, uint8_t* recv, uint64_t chunk);
+int kgs_group_create_host_a2a(int world, kgs_allgather_fn fn, kgs_alltoall_fn a2a, void* user, kgs_group_t** out);
 int kgs_group_rccl_unique_id(uint8_t id[128]);
 int kgs_group_create_rccl(int rank, int world, const uint8_t id[128], int device, kgs_group_t** out);
 void kgs_group_destroy(kgs_group_t* g);
@@ -125,6 +131,11 @@ int kgs_group_world(kgs_group_t* g, int* world);
 /* attach (g != NULL) or detach (g == NULL) the distributed prover for this rank; a world-1 group
  * runs the distributed code path on one rank (exercises a transport end to end on one GPU) */
 int kgs_ctx_set_group(kgs_ctx_t* ctx, kgs_group_t* g, int rank);
+/* exchanges of the context's last proof (zeros after a single-GPU proof): out[0..5] = all-to-all
+ * count, their summed span in ms (HIP events on the prover's stream around each exchange: the
+ * transfer plus any wait for the peers), bytes that left this rank in them; host all-gather count,
+ * their summed wall ms, bytes sent (bytes x (world - 1)). Returns the number of values written. */
+int kgs_last_exchange(kgs_ctx_t* ctx, double* out, int max);
 
 /* MSM lanes per context (default 2): with 2, the independent commitments of one prover round
  * (round 1's F_i / T_i, round 5's W_xi / W_xiw) alternate between two HIP streams with separate

@@ -115,6 +115,9 @@ def lib():
         L.kgs_group_create_local.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
         L.kgs_group_create_host.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.POINTER(ctypes.c_void_p)]
+        L.kgs_group_create_host_a2a.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.POINTER(ctypes.c_void_p)]
+        L.kgs_last_exchange.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.kgs_group_rccl_unique_id.argtypes = [c_u8p]
         L.kgs_group_create_rccl.argtypes = [ctypes.c_int, ctypes.c_int, c_u8p, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_void_p)]
@@ -128,6 +131,8 @@ def lib():
 
 # int (*kgs_allgather_fn)(void* user, const uint8_t* send, uint8_t* recv, uint64_t bytes)
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+# int (*kgs_alltoall_fn)(void* user, const uint8_t* send, uint8_t* recv, uint64_t chunk)
+ALLTOALL_FN = ALLGATHER_FN
 
 
 def _check(rc):
@@ -236,12 +241,30 @@ def torch_allgather(group=None, device=None):
     return fn
 
 
+def torch_alltoall(group=None):
+    """All-to-all transport for Group.host over torch.distributed (all_to_all_single on host tensors:
+    gloo): alltoall(data, chunk) sends chunk j of `data` to rank j and returns the world chunks
+    received, rank-major."""
+    import torch
+    import torch.distributed as dist
+
+    def fn(data, chunk):
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        out = torch.empty_like(t)
+        dist.all_to_all_single(out, t, group=group)
+        return out.numpy().tobytes()
+    return fn
+
+
 class Group:
     """Rank group of the distributed prover (kgs_group_t; Context.set_group): every vector of a
     proof sharded over `world` ranks, one context per rank.
       Group.local(world)                 several contexts of this process (one host thread per rank)
-      Group.host(world, allgather)       any host all-gather(bytes) -> world * bytes (e.g. gloo);
-                                         device data is staged through the host
+      Group.host(world, allgather[, alltoall])
+                                         any host all-gather(bytes) -> world * bytes (e.g. gloo) and,
+                                         optionally, an all-to-all(bytes, chunk) -> bytes (chunk j to
+                                         rank j: (W - 1) / W of a vector leaves a rank instead of every
+                                         rank receiving W x it); device data is staged through the host
       Group.rccl(rank, world, id, dev)   one process per GPU, RCCL over xGMI; id = rccl_unique_id()
                                          made on rank 0 and broadcast by the caller"""
 
@@ -257,7 +280,7 @@ class Group:
         return cls(h, world)
 
     @classmethod
-    def host(cls, world, allgather):
+    def host(cls, world, allgather, alltoall=None):
         def _cb(user, send, recv, nbytes):
             try:
                 out = allgather(ctypes.string_at(send, nbytes))
@@ -269,10 +292,27 @@ class Group:
                 import traceback
                 traceback.print_exc()
                 return -1
+
+        def _a2a(user, send, recv, chunk):
+            try:
+                out = alltoall(ctypes.string_at(send, chunk * world), chunk)
+                if len(out) != chunk * world:
+                    return -1
+                ctypes.memmove(recv, out, len(out))
+                return 0
+            except Exception:
+                import traceback
+                traceback.print_exc()
+                return -1
         cb = ALLGATHER_FN(_cb)
         h = ctypes.c_void_p()
-        _check(lib().kgs_group_create_host(world, ctypes.cast(cb, ctypes.c_void_p), None, ctypes.byref(h)))
-        return cls(h, world, cb)
+        if alltoall is None:
+            _check(lib().kgs_group_create_host(world, ctypes.cast(cb, ctypes.c_void_p), None, ctypes.byref(h)))
+            return cls(h, world, cb)
+        cb2 = ALLTOALL_FN(_a2a)
+        _check(lib().kgs_group_create_host_a2a(world, ctypes.cast(cb, ctypes.c_void_p), ctypes.cast(cb2, ctypes.c_void_p),
+                                               None, ctypes.byref(h)))
+        return cls(h, world, (cb, cb2))
 
     @classmethod
     def rccl(cls, rank, world, uid, device):
@@ -474,6 +514,14 @@ class Context:
         _check(lib().kgs_poly_div_x_sub(self._h, _buf(coef_mont), len(coef_mont) // 32, _buf(z_mont), out))
         return out.raw
 
+    def last_exchange(self):
+        """Exchanges of the last proof (kgs_last_exchange): all-to-all count / summed span ms / bytes
+        sent, host all-gather count / wall ms / bytes sent; zeros after a single-GPU proof."""
+        arr = (ctypes.c_double * 6)()
+        lib().kgs_last_exchange(self._h, arr, 6)
+        return {"alltoall_n": int(arr[0]), "alltoall_ms": arr[1], "alltoall_bytes": int(arr[2]),
+                "allgather_n": int(arr[3]), "allgather_ms": arr[4], "allgather_bytes": int(arr[5])}
+
     def last_timing(self):
         arr = (ctypes.c_double * 9)()
         n = lib().kgs_last_timing(self._h, arr, 9)
@@ -540,6 +588,22 @@ class Context:
         _check(lib().kgs_prove_device(self._h, kind, nbits, k, PF, PT, d_sf, d_st, com, ev))
         return ([com.raw[64 * i:64 * i + 64] for i in range(nc.value)],
                 [ev.raw[32 * i:32 * i + 32] for i in range(ne.value)])
+
+
+def dist_exchange_model(kind, nbits, npols, selected, world):
+    """All-to-alls of one distributed proof (csrc/prover_dist.cpp) and the bytes that
+    leave each rank in them: round 1 one per F_i / T_i (+ selectors) at n; round 2 S BLOCK -> E and its
+    inverse at n, the coset forward transforms of S, F, T (+ selectors) at the coset size cs; round 3
+    the quotient's inverse at cs; round 5 the two numerators CYCLIC -> BLOCK and the two openings
+    BLOCK -> CYCLIC (one at cs, one at n each). An all-to-all of a length-L vector sends L / W^2
+    elements to each of the W - 1 other ranks."""
+    n = 1 << nbits
+    gs = kind != GRANDPRODUCT
+    cs = n if (not gs and not selected) else 2 * n
+    sel = 2 if selected else 0
+    lens = [n] * (2 * npols + sel) + [n, n] + [cs] * (3 + sel) + [cs] + [cs, n, cs, n]
+    W = world
+    return {"alltoall_n": len(lens), "alltoall_bytes": sum(32 * (L // (W * W)) * (W - 1) for L in lens)}
 
 
 def proof_names(kind, npols, selected):

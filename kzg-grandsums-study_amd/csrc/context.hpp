@@ -148,6 +148,27 @@ struct kgs_group {
 // seconds a rank waits for its peers in a group exchange (KGS_GROUP_TIMEOUT_S, default 120)
 double group_timeout_s();
 
+// Exchanges of the last distributed proof on a context (kgs_last_exchange): every all-to-all is
+// bracketed by two events on the stream it is ordered on (its span includes waiting for the peers),
+// every host all-gather by the wall clock; bytes are those leaving this rank.
+struct ExchangeStats {
+  int a2a_n = 0, ag_n = 0;
+  double a2a_ms = 0, ag_ms = 0;
+  uint64_t a2a_bytes = 0, ag_bytes = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;  // grow-only pool
+  void reset() {
+    a2a_n = ag_n = 0;
+    a2a_ms = ag_ms = 0;
+    a2a_bytes = ag_bytes = 0;
+  }
+  ~ExchangeStats() {
+    for (auto& e : ev) {
+      hipEventDestroy(e.first);
+      hipEventDestroy(e.second);
+    }
+  }
+};
+
 struct kgs_ctx {
   // every C-ABI entry point that touches the context holds mu: a busy context blocks its caller,
   // it is never entered twice (the JS backend runs prove() calls on libuv worker threads)
@@ -203,6 +224,7 @@ struct kgs_ctx {
   int group_rank = 0;
   int srs_slice_rank = 0, srs_slice_world = 1;  // of the loaded SRS (SrsTables::slice_*)
   std::map<std::string, uint32_t*> dist_tabs;  // per-rank coset / 1/(n(x-1)) tables (pool buffers)
+  ExchangeStats xs;                             // exchanges of the last distributed proof
 
   ~kgs_ctx() {
     hipSetDevice(device);

@@ -70,6 +70,8 @@ void launch_bitrev_copy(hipStream_t st, uint32_t* out, const uint32_t* in, int l
 
 // poly.hip
 void launch_to_mont(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t n);
+// device -> mapped pinned host memory by a small store kernel (bytes a multiple of 16)
+void launch_host_store(hipStream_t st, void* dst_host_mapped, const void* src, uint64_t bytes, unsigned blocks);
 void launch_lincomb(hipStream_t st, uint32_t* out, uint64_t n, const LinComb& lc);
 void launch_builder(hipStream_t st, bool prod, bool sel, uint32_t* out, const uint32_t* f, const uint32_t* t,
                     const uint32_t* sf, const uint32_t* stt, const uint32_t* gamma, uint64_t n, uint32_t* scratch_tp,

@@ -38,6 +38,20 @@ __global__ void k_to_mont(uint32_t* __restrict__ out, const uint32_t* __restrict
 void launch_to_mont(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t n) {
   hipLaunchKernelGGL(k_to_mont, dim3(nb(n)), dim3(256), 0, st, out, in, n);
 }
+// Device -> pinned host copy by the shader (the Montgomery write-back, prover.js:147-148): 16-byte
+// non-temporal stores straight into the mapped host buffer from a small grid-stride grid. The copy is
+// PCIe-bound (~52 GB/s, profiles/ubench/d2h_engine.hip); hipMemcpyAsync D2H ran either on an SDMA
+// engine at ~30 GB/s or, with several proofs in flight, as the runtime's __amd_rocclr_copyBuffer blit
+// kernel (256 x 512 threads for 0.8 ms per 32 MiB) whose waves kept the other proofs' kernels from
+// co-residing. Few blocks and few VGPRs: the waves mostly wait on their stores.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) k_host_store(u32x4* __restrict__ dst, const u32x4* __restrict__ src, uint64_t n16) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
+    __builtin_nontemporal_store(src[i], &dst[i]);
+}
+void launch_host_store(hipStream_t st, void* dst_host_mapped, const void* src, uint64_t bytes, unsigned blocks) {
+  hipLaunchKernelGGL(k_host_store, dim3(blocks), dim3(256), 0, st, (u32x4*)dst_host_mapped, (const u32x4*)src, bytes / 16);
+}
 // [ffjs] Fr.batchFromMontgomery (polynomial.js:1112, before G1.multiExpAffine)
 __global__ void k_from_mont(uint32_t* __restrict__ out, const uint32_t* __restrict__ in, uint64_t n) {
   KGS_AUX_PRIO();

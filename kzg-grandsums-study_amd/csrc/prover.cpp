@@ -308,6 +308,28 @@ void load_points(kgs_ctx& c, const uint8_t* lem, uint64_t npts, int power, int n
 // T_k (XYZZ) -> host sum_k 2^k T_k -> affine LEM. Sharded (world > 1): this rank's point range
 // only; the partials of all ranks are all-gathered once per batch of commits (one prover round).
 
+// The host-boundary copy streams (st_copy: input DMAs, st_wb: the Montgomery write-back) carry only
+// copies and event waits. HIP maps streams onto a few hardware queues per priority level
+// (GPU_MAX_HW_QUEUES, 4 by default), so with several contexts in flight a copy stream would share a
+// hardware queue with another proof's compute stream, whose kernels then queue behind the copy
+// stream's waits. Created at the lowest priority they get their own pool of hardware queues
+// (KGS_COPY_STREAM_PRIO=normal keeps them in the compute streams' pool, for A/B).
+hipStream_t copy_stream() {
+  static const bool low = [] {
+    const char* e = getenv("KGS_COPY_STREAM_PRIO");
+    return !(e && !strcmp(e, "normal"));
+  }();
+  hipStream_t s = nullptr;
+  if (low) {
+    int least = 0, greatest = 0;
+    HC(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HC(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, least));
+  } else {
+    HC(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  }
+  return s;
+}
+
 void shard_range(uint64_t n, int rank, int world, uint64_t& lo, uint64_t& hi) {
   lo = (uint64_t)((unsigned __int128)n * (unsigned)rank / (unsigned)world);
   hi = (uint64_t)((unsigned __int128)n * (unsigned)(rank + 1) / (unsigned)world);
@@ -589,6 +611,7 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     throw KgsError(KGS_E_ARG, "unknown argument kind");
   if (in.kind == KGS_LOOKUP && !in.sel_f)
     throw KgsError(KGS_E_ARG, "a lookup needs both selectors (sel_t holds the multiplicities)");
+  c.xs.reset();
   if (c.group) {
     if (c.ref_quirks && in.kind != KGS_LOOKUP)
       throw KgsError(KGS_E_ARG, "reference-quirks mode runs on the single-GPU prover only");
@@ -671,7 +694,7 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   int nwb = 0;
   auto write_back = [&](uint8_t* dst, const uint32_t* src, hipStream_t st) {
     if (!dst) return;
-    if (!c.st_wb) HC(hipStreamCreateWithFlags(&c.st_wb, hipStreamNonBlocking));
+    if (!c.st_wb) c.st_wb = copy_stream();
     if ((int)c.ev_wb.size() <= nwb) {
       hipEvent_t e;
       HC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -680,7 +703,22 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     HC(hipEventRecord(c.ev_wb[nwb], st));
     HC(hipStreamWaitEvent(c.st_wb, c.ev_wb[nwb], 0));
     nwb++;
-    HC(hipMemcpyAsync(dst, src, E, hipMemcpyDeviceToHost, c.st_wb));
+    // hipMemcpyAsync (an SDMA engine: no CU time). KGS_WB_COPY=kernel stores from a shader into the
+    // mapped pinned buffer instead (poly.hip k_host_store): measured slower in flight, 83-85 vs 86-88
+    // proofs/s (profiles/r05/wb_ab.txt), kept for A/B
+    static const unsigned wb_blocks = [] {
+      const char* e = getenv("KGS_WB_COPY");
+      if (!(e && !strcmp(e, "kernel"))) return 0u;
+      const char* b = getenv("KGS_WB_BLOCKS");
+      return b ? (unsigned)atoi(b) : 64u;
+    }();
+    void* mapped = nullptr;
+    if (wb_blocks && hipHostGetDevicePointer(&mapped, dst, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      mapped = nullptr;
+    }
+    if (mapped && E % 16 == 0) launch_host_store(c.st_wb, mapped, src, E, wb_blocks);
+    else HC(hipMemcpyAsync(dst, src, E, hipMemcpyDeviceToHost, c.st_wb));
   };
   auto mont_out = [&](const std::vector<uint8_t*>& v, int i) -> uint8_t* { return v.empty() ? nullptr : v[i]; };
   std::vector<Commit> r1;
@@ -1300,6 +1338,16 @@ namespace kgsi {
 // helpers are a persistent pool (spawning 8-16 threads per call cost ~0.1 ms, paid several times per
 // proof once inputs are fed in pieces); the calling thread copies too, so a busy pool never stalls it.
 static std::atomic<int> g_copy_active{0};
+// host threads for the staging copies of all contexts together (KGS_COPY_THREADS, default 16: a GPU's
+// share of the host's cores)
+static unsigned copy_threads() {
+  static const unsigned n = [] {
+    const char* e = getenv("KGS_COPY_THREADS");
+    const int v = e ? atoi(e) : 16;
+    return (unsigned)(v >= 1 && v <= 64 ? v : 16);
+  }();
+  return n;
+}
 namespace {
 struct CopyTask {
   std::vector<CopyJob> pieces;
@@ -1338,7 +1386,7 @@ struct CopyPool {  // leaked on purpose: its detached threads outlive static des
       }).detach();
   }
   static CopyPool& get() {
-    static CopyPool* p = new CopyPool(16);
+    static CopyPool* p = new CopyPool(copy_threads());
     return *p;
   }
 };
@@ -1355,7 +1403,7 @@ void par_copy(const std::vector<CopyJob>& jobs) {
     ~Active() { g_copy_active.fetch_sub(1); }
   } active;
   unsigned nth = std::thread::hardware_concurrency();
-  nth = std::max(1u, std::min(nth, 16u) / (unsigned)std::max(1, active.n));
+  nth = std::max(1u, std::min(nth, copy_threads()) / (unsigned)std::max(1, active.n));
   nth = std::min<unsigned>(nth, (unsigned)task->pieces.size());
   if (nth > 1) {
     CopyPool& pool = CopyPool::get();
@@ -1529,7 +1577,7 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
     // zero-copy: every input DMA'd straight from the caller's pinned buffer, one after the other on the
     // copy stream (not two streams at once: F_0 then arrives after one vector's transfer time instead
     // of sharing the link with T_0), each with the event its first kernel waits for
-    if (!ctx->st_copy) HC(hipStreamCreateWithFlags(&ctx->st_copy, hipStreamNonBlocking));
+    if (!ctx->st_copy) ctx->st_copy = copy_stream();
     while (ctx->ev_in.size() < in_jobs.size()) {
       hipEvent_t e;
       HC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1551,7 +1599,7 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
     // waits for right before the vector's first kernel, so F_0's transform starts while the rest
     // are still in flight. (The Montgomery write-back later reuses the same pinned slots on the
     // copy stream, after these DMAs in stream order.)
-    if (!ctx->st_copy) HC(hipStreamCreateWithFlags(&ctx->st_copy, hipStreamNonBlocking));
+    if (!ctx->st_copy) ctx->st_copy = copy_stream();
     while (ctx->ev_in.size() < in_jobs.size()) {
       hipEvent_t e;
       HC(hipEventCreateWithFlags(&e, hipEventDisableTiming));

@@ -130,23 +130,35 @@ struct LocalGroup : kgs_group {
   }
 };
 
-// any host all-gather callback (torch.distributed, gloo, MPI ...): device data staged through the host
+// host callbacks (torch.distributed gloo, MPI ...): device data staged through the host. With an
+// all-to-all callback each rank sends chunk j to rank j and receives one chunk from each rank
+// ((W - 1) / W of its vector leaves it); with only the all-gather, every rank receives every rank's
+// whole vector (W x the data) and keeps its chunks.
 struct HostGroup : kgs_group {
   kgs_allgather_fn fn;
+  kgs_alltoall_fn a2a_fn;
   void* user;
-  HostGroup(int w, kgs_allgather_fn f, void* u) : fn(f), user(u) { world = w; }
+  std::vector<uint8_t> h_send, h_recv;
+  HostGroup(int w, kgs_allgather_fn f, kgs_alltoall_fn a, void* u) : fn(f), a2a_fn(a), user(u) { world = w; }
   void allgather(int, const void* send, void* recv, size_t bytes) override {
     if (fn(user, (const uint8_t*)send, (uint8_t*)recv, bytes) != 0) throw KgsError(KGS_E_COMM, "group all-gather failed");
   }
   void alltoall(int rank, kgs_ctx&, hipStream_t st, const void* send, void* recv, size_t chunk) override {
     const size_t bytes = chunk * world;
-    std::vector<uint8_t> h(bytes), all(bytes * world);
-    HC(hipMemcpyAsync(h.data(), send, bytes, hipMemcpyDeviceToHost, st));
+    if (h_send.size() < bytes) h_send.resize(bytes);
+    HC(hipMemcpyAsync(h_send.data(), send, bytes, hipMemcpyDeviceToHost, st));
     HC(hipStreamSynchronize(st));
-    allgather(rank, h.data(), all.data(), bytes);
-    for (int j = 0; j < world; j++)
-      HC(hipMemcpyAsync((uint8_t*)recv + (size_t)j * chunk, all.data() + (size_t)j * bytes + (size_t)rank * chunk, chunk,
-                        hipMemcpyHostToDevice, st));
+    if (a2a_fn) {
+      if (h_recv.size() < bytes) h_recv.resize(bytes);
+      if (a2a_fn(user, h_send.data(), h_recv.data(), (uint64_t)chunk) != 0) throw KgsError(KGS_E_COMM, "group all-to-all failed");
+      HC(hipMemcpyAsync(recv, h_recv.data(), bytes, hipMemcpyHostToDevice, st));
+    } else {
+      if (h_recv.size() < bytes * world) h_recv.resize(bytes * world);
+      allgather(rank, h_send.data(), h_recv.data(), bytes);
+      for (int j = 0; j < world; j++)
+        HC(hipMemcpyAsync((uint8_t*)recv + (size_t)j * chunk, h_recv.data() + (size_t)j * bytes + (size_t)rank * chunk,
+                          chunk, hipMemcpyHostToDevice, st));
+    }
     HC(hipStreamSynchronize(st));
   }
 };
@@ -246,8 +258,38 @@ struct Dist {
   const int W, r, logW;
   Dist(kgs_ctx& cc) : c(cc), g(*cc.group), W(cc.group->world), r(cc.group_rank), logW(ilog2(cc.group->world)) {}
 
+  // every exchange is counted in c.xs (kgs_last_exchange): all-to-alls by two events on the stream,
+  // host all-gathers by the wall clock; bytes leaving this rank
   void a2a(const uint32_t* send, uint32_t* recv, uint64_t chunk_elems) {
+    ExchangeStats& x = c.xs;
+    if ((int)x.ev.size() <= x.a2a_n) {
+      hipEvent_t e0, e1;
+      HC(hipEventCreate(&e0));
+      HC(hipEventCreate(&e1));
+      x.ev.push_back({e0, e1});
+    }
+    const auto& ev = x.ev[x.a2a_n++];
+    HC(hipEventRecord(ev.first, c.st));
     g.alltoall(r, c, c.st, send, recv, (size_t)32 * chunk_elems);
+    HC(hipEventRecord(ev.second, c.st));
+    x.a2a_bytes += (uint64_t)32 * chunk_elems * (W - 1);
+  }
+  void allgather(const void* s, void* rv, size_t b) {
+    const auto t0 = std::chrono::steady_clock::now();
+    g.allgather(r, s, rv, b);
+    c.xs.ag_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c.xs.ag_n++;
+    c.xs.ag_bytes += (uint64_t)b * (W - 1);
+  }
+  // after the proof's last sync: the all-to-all spans from their events
+  void finish_stats() {
+    ExchangeStats& x = c.xs;
+    x.a2a_ms = 0;
+    for (int i = 0; i < x.a2a_n; i++) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, x.ev[i].first, x.ev[i].second) == hipSuccess) x.a2a_ms += ms;
+      else (void)hipGetLastError();
+    }
   }
   // per-rank coset tables g^(+-(r + W i)), i < Ml, cached by (sign, logMl)
   uint32_t* coset_tab(int logMl, bool inverse) {
@@ -310,20 +352,20 @@ struct Dist {
   std::vector<Fr> gather_fr(const std::vector<Fr>& mine) {
     std::vector<uint8_t> s(32 * mine.size()), all(32 * mine.size() * W);
     for (size_t i = 0; i < mine.size(); i++) mine[i].to_bytes(s.data() + 32 * i);
-    g.allgather(r, s.data(), all.data(), s.size());
+    allgather(s.data(), all.data(), s.size());
     std::vector<Fr> out(mine.size() * W);
     for (size_t i = 0; i < out.size(); i++) out[i] = Fr::from_bytes(all.data() + 32 * i);
     return out;  // rank-major
   }
   uint32_t gather_or(uint32_t mine) {
     std::vector<uint32_t> all(W);
-    g.allgather(r, &mine, all.data(), 4);
+    allgather(&mine, all.data(), 4);
     uint32_t o = 0;
     for (uint32_t v : all) o |= v;
     return o;
   }
   HostAllgather host_ag() {
-    return [this](const void* s, void* rv, size_t b) { g.allgather(r, s, rv, b); };
+    return [this](const void* s, void* rv, size_t b) { allgather(s, rv, b); };
   }
 };
 
@@ -596,7 +638,7 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
   HC(hipMemcpyAsync(h_heads, heads, (size_t)32 * rot * W, hipMemcpyDeviceToHost, c.st));
   HC(hipStreamSynchronize(c.st));
   std::vector<uint8_t> all_heads((size_t)32 * rot * W * W);
-  D.g.allgather(r, h_heads, all_heads.data(), (size_t)32 * rot * W);
+  D.allgather(h_heads, all_heads.data(), (size_t)32 * rot * W);
   uint8_t* h_halo = c.pin((size_t)32 * rot * W);
   for (int k1 = 0; k1 < W; k1++) {
     const int src = r + 1 < W ? r + 1 : 0;
@@ -775,6 +817,7 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
   for (int i = 0; i < ncom_all; i++) memcpy(com_out + 64 * i, com[i].data(), 64);
   for (size_t i = 0; i < evals.size(); i++) evals[i].to_bytes(ev_out + 32 * i);
   c.reset_staging();
+  D.finish_stats();
 }
 
 // Preconditions are agreed by all ranks (dist_preconditions: they all throw together, the group
@@ -783,6 +826,7 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
 // that the other ranks fail at their next exchange instead of waiting in it (RCCL: at the
 // KGS_GROUP_TIMEOUT_S deadline of RcclGroup::wait).
 void prove_dist_group(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out) {
+  c.xs.reset();
   dist_preconditions(c, in);
   try {
     prove_dist_impl(c, in, com_out, ev_out);
@@ -829,8 +873,26 @@ int kgs_group_create_host(int world, kgs_allgather_fn fn, void* user, kgs_group_
   API_BEGIN
   if (!out || !fn) throw KgsError(KGS_E_ARG, "NULL argument");
   check_world(world);
-  *out = new HostGroup(world, fn, user);
+  *out = new HostGroup(world, fn, nullptr, user);
   API_END
+}
+
+int kgs_group_create_host_a2a(int world, kgs_allgather_fn fn, kgs_alltoall_fn a2a, void* user, kgs_group_t** out) {
+  API_BEGIN
+  if (!out || !fn || !a2a) throw KgsError(KGS_E_ARG, "NULL argument");
+  check_world(world);
+  *out = new HostGroup(world, fn, a2a, user);
+  API_END
+}
+
+int kgs_last_exchange(kgs_ctx_t* ctx, double* out, int max) {
+  if (!ctx || !out) return KGS_E_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  const ExchangeStats& x = ctx->xs;
+  const double v[6] = {(double)x.a2a_n, x.a2a_ms, (double)x.a2a_bytes, (double)x.ag_n, x.ag_ms, (double)x.ag_bytes};
+  const int n = max < 6 ? max : 6;
+  for (int i = 0; i < n; i++) out[i] = v[i];
+  return n;
 }
 
 int kgs_group_rccl_unique_id(uint8_t id[128]) {
