@@ -176,7 +176,13 @@ struct kgs_ctx {
   int device = 0;
   hipStream_t st = nullptr;
   std::map<std::string, DBuf> pool;
-  // pinned staging of the host-buffer boundary (kgs_prove's inputs and Montgomery write-back)
+  // pinned staging of the host-buffer boundary: h_in receives kgs_prove's inputs (the CPU only writes
+  // it, the DMA engine reads it), h_io the Montgomery write-back (the CPU reads it). KGS_STAGE_WC=1
+  // makes h_in write-combined: SDMA reads that at ~55 GB/s against ~30 GB/s from coherent pinned
+  // memory alone (profiles/r05/d2h_engine.txt), but the host copy into it is slower and a proof
+  // measured the same either way (profiles/r05/stage_wc_ab.txt), so it is off by default
+  uint8_t* h_in = nullptr;
+  size_t h_in_bytes = 0;
   uint8_t* h_io = nullptr;
   size_t h_io_bytes = 0;
   // pinned staging
@@ -236,6 +242,7 @@ struct kgs_ctx {
     for (auto& kv : pool) hipFree(kv.second.p);
     if (h_pin) hipHostFree(h_pin);
     if (h_io) hipHostFree(h_io);
+    if (h_in) hipHostFree(h_in);
     if (ev_fork) hipEventDestroy(ev_fork);
     if (ev_join) hipEventDestroy(ev_join);
     for (hipEvent_t e : ev_in) hipEventDestroy(e);
@@ -266,6 +273,23 @@ struct kgs_ctx {
       b.bytes = sz;
     }
     return (uint32_t*)b.p;
+  }
+  uint8_t* io_in(size_t bytes) {
+    if (h_in_bytes < bytes) {
+      if (h_in) {
+        sync();
+        HC(hipHostFree(h_in));
+        h_in = nullptr;
+        h_in_bytes = 0;
+      }
+      static const bool wc = [] {
+        const char* e = getenv("KGS_STAGE_WC");
+        return e && !strcmp(e, "1");
+      }();
+      HC(hipHostMalloc((void**)&h_in, bytes, wc ? hipHostMallocWriteCombined : hipHostMallocDefault));
+      h_in_bytes = bytes;
+    }
+    return h_in;
   }
   uint8_t* io(size_t bytes) {
     if (h_io_bytes < bytes) {

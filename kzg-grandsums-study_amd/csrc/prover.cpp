@@ -1520,18 +1520,20 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   in.kind = kind;
   in.nbits = nbits;
   in.npols = npols;
-  // pageable caller buffers -> pinned staging (parallel host copies) -> one DMA per vector; the
-  // Montgomery write-back goes device -> the same pinned slots -> caller (after the proof)
+  // pageable caller buffers -> write-combined pinned staging (parallel host copies) -> DMAs; the
+  // Montgomery write-back goes device -> its own pinned slots (st_wb) -> caller (a host thread)
   const int nvec = 2 * npols + (sel_f ? 2 : 0);
-  uint8_t* pio = ctx->io((size_t)nvec * E);
+  uint8_t* pin_in = ctx->io_in((size_t)nvec * E);
+  const bool any_wb = mont_f || mont_t;
+  uint8_t* pio = any_wb ? ctx->io((size_t)2 * npols * E) : nullptr;  // write-back slots
   std::vector<CopyJob> in_jobs;
   for (int i = 0; i < npols; i++) {
-    in_jobs.push_back({pio + (size_t)(2 * i) * E, evals_f[i], E});
-    in_jobs.push_back({pio + (size_t)(2 * i + 1) * E, evals_t[i], E});
+    in_jobs.push_back({pin_in + (size_t)(2 * i) * E, evals_f[i], E});
+    in_jobs.push_back({pin_in + (size_t)(2 * i + 1) * E, evals_t[i], E});
   }
   if (sel_f) {
-    in_jobs.push_back({pio + (size_t)(2 * npols) * E, sel_f, E});
-    in_jobs.push_back({pio + (size_t)(2 * npols + 1) * E, sel_t, E});
+    in_jobs.push_back({pin_in + (size_t)(2 * npols) * E, sel_f, E});
+    in_jobs.push_back({pin_in + (size_t)(2 * npols + 1) * E, sel_t, E});
   }
   ctx->sync();  // the staging area may still feed a previous call's copies
   // inputs: one parallel host copy into the pinned slots, then one DMA per vector
@@ -1597,8 +1599,9 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
     // pipelined: vector v's host copy into its pinned slot overlaps vector v - 1's DMA; vector 0
     // goes on the main stream, the others on the copy stream with an event that the main stream
     // waits for right before the vector's first kernel, so F_0's transform starts while the rest
-    // are still in flight. (The Montgomery write-back later reuses the same pinned slots on the
-    // copy stream, after these DMAs in stream order.)
+    // are still in flight. (The Montgomery write-back has pinned slots of its own, written on st_wb:
+    // vector v's D2H is ordered after its conversion kernel, which waits on ev_in[v], i.e. after
+    // vector v's input DMA.)
     if (!ctx->st_copy) ctx->st_copy = copy_stream();
     while (ctx->ev_in.size() < in_jobs.size()) {
       hipEvent_t e;
