@@ -144,20 +144,23 @@ int kgs_last_exchange(kgs_ctx_t* ctx, double* out, int max);
  * keep the GPU busy with independent proofs (throughput). */
 int kgs_ctx_set_msm_lanes(kgs_ctx_t* ctx, int lanes);
 
-/* Reference-quirks mode (default off; a new context starts with the value of the environment variable
- * KGS_REFERENCE_QUIRKS, "1" = on). Off, the prover returns a valid proof for every valid multiset. On,
- * it reproduces what the reference does on the degenerate inputs where the reference does not
- * compute the mathematical quotient (DESIGN.md §4 "Reference quirks"):
+/* Reference-quirks mode (default ON since round 5: a new context is on unless the environment variable
+ * KGS_REFERENCE_QUIRKS is "0"). On, the prover reproduces what the reference does on the degenerate
+ * inputs where the reference does not compute the mathematical quotient (DESIGN.md §4 "Reference
+ * quirks"); off (exact-math mode), it returns a valid proof for every valid
+ * multiset. Detecting the degenerate inputs costs nothing measurable (93.0 proofs/s either way at
+ * n = 2^20, profiles/r05/quirks_cost_ab.txt):
  *   - an operand of degree 1 <= d < n/2 (F, T, S/Z, selF, selT — e.g. F[i] = w^i): the reference's
  *     Polynomial.multiply evaluates it on the wrong points (polynomial.js:352-376 vs
  *     evaluations.js:12-18); the reference's quotient chain is then replayed on the GPU with the
  *     reference's buffer sizes and buffer sharing, and the prover fails where the reference fails
  *     ("Polynomial is not divisible", "Polynomial does not divide") or returns the proof it returns;
  *   - a zero quotient (e.g. F == T element by element): KGS_E_RANGE "offset is out of bounds".
- * Only the two reference arguments are affected (KGS_LOOKUP has no reference behaviour to follow) and
- * only the single-GPU prover (a context attached to a group fails with KGS_E_ARG). The replay
- * reproduces transforms of up to 2^26 points (the reference's own need n^2 points for a degree-1
- * operand); beyond that it fails with KGS_E_ARG. */
+ * Only the two reference arguments are affected (KGS_LOOKUP has no reference behaviour to follow). A
+ * rank group (kgs_ctx_set_group) decides the degenerate cases from all-gathered degrees and replays
+ * the chain on the gathered operands on every rank: every rank fails with the reference's error, or
+ * returns the reference's proof. The replay reproduces transforms of up to 2^26 points (the
+ * reference's own need n^2 points for a degree-1 operand); beyond that it fails with KGS_E_ARG. */
 int kgs_ctx_set_reference_quirks(kgs_ctx_t* ctx, int on);
 
 /* Load a .ptau file (binfileutils layout, sections 1-3) and make the first 2^(nbits_max+1) G1

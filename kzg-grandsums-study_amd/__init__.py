@@ -405,8 +405,9 @@ class Context:
         return self._h
 
     def set_reference_quirks(self, on):
-        """Reference-quirks mode (kgs_ctx_set_reference_quirks; default: env KGS_REFERENCE_QUIRKS == "1"):
-        reproduce the reference's failures on degenerate inputs instead of proving them."""
+        """Reference-quirks mode (kgs_ctx_set_reference_quirks; default ON unless the environment has
+        KGS_REFERENCE_QUIRKS == "0"): reproduce the reference's failures on degenerate inputs; off, the
+        exact-math prover proves them."""
         _check(lib().kgs_ctx_set_reference_quirks(self._h, 1 if on else 0))
 
     def set_msm_lanes(self, lanes):
@@ -682,7 +683,7 @@ def _prover(kind, pTauFilename, evalsFs, evalsTs, evalsSelF=None, evalsSelT=None
             log.info(line)
     ctx = _context(device)
     # the drop-in functions follow the environment on every call (contexts are cached per device)
-    ctx.set_reference_quirks(os.environ.get("KGS_REFERENCE_QUIRKS") == "1")
+    ctx.set_reference_quirks(os.environ.get("KGS_REFERENCE_QUIRKS", "1") != "0")
     # only the 2^(nbits+1) points this proof commits with (prover.js:83-85); grow-only device cache
     ctx.load_ptau(pTauFilename, nbits)
     coms, evs, mf, mt = ctx.prove(kind, nbits, [e.eval for e in evalsFs], [e.eval for e in evalsTs],

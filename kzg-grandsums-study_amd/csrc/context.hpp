@@ -213,7 +213,7 @@ struct kgs_ctx {
   std::vector<hipEvent_t> ev_in;  // kgs_prove: one per input vector DMA'd on the copy stream
   MsmWork mw2;
   int msm_lanes = 2;  // kgs_ctx_set_msm_lanes
-  bool ref_quirks = false;  // kgs_ctx_set_reference_quirks (ref_quirks.cpp)
+  bool ref_quirks = true;  // kgs_ctx_set_reference_quirks (ref_quirks.cpp); default on
   uint64_t msm_nseg_max = 0;
   // domain tables (M = 2^logM; shared) and this context's views of them
   std::shared_ptr<DomainTables> dom;
@@ -231,6 +231,7 @@ struct kgs_ctx {
   int srs_slice_rank = 0, srs_slice_world = 1;  // of the loaded SRS (SrsTables::slice_*)
   std::map<std::string, uint32_t*> dist_tabs;  // per-rank coset / 1/(n(x-1)) tables (pool buffers)
   ExchangeStats xs;                             // exchanges of the last distributed proof
+  bool dist_err_agreed = false;  // the distributed proof's current failure is the same on every rank
 
   ~kgs_ctx() {
     hipSetDevice(device);
@@ -380,8 +381,10 @@ void coset_fwd(kgs_ctx& c, uint32_t* out, const uint32_t* in, uint64_t len, int 
 void coset_inv_prescaled(kgs_ctx& c, uint32_t* out, const uint32_t* in, int lcs);
 
 // reference-quirks mode (ref_quirks.cpp; kgs_ctx_set_reference_quirks)
-bool ref_quirks_needed(kgs_ctx& c, uint64_t n, const std::vector<const uint32_t*>& ops);
-bool ref_quotient_is_zero(kgs_ctx& c, const uint32_t* Q, uint64_t qlen);
+uint32_t* ref_quirks_probe(kgs_ctx& c, uint64_t n, const std::vector<const uint32_t*>& ops, const uint32_t* Q,
+                           uint64_t qlen);
+bool ref_quirks_needed(const uint32_t* probe, size_t nops, uint64_t n);
+bool ref_quotient_is_zero(const uint32_t* probe);
 uint32_t* ref_quirks_quotient(kgs_ctx& c, bool gs, bool sel, bool lookup, int nbits, const Fr& alpha, const Fr& gamma,
                               const uint32_t* dF, const uint32_t* dT, const uint32_t* dS, const uint32_t* dSF,
                               const uint32_t* dST, uint64_t& qlen, uint32_t*& fmut);

@@ -637,22 +637,39 @@ void launch_nxm1(hipStream_t st, uint32_t* out, const uint32_t* tw, uint64_t hal
 // (kgs_ctx_set_reference_quirks; prover.cpp ref_quirks_quotient). Not on the default path: these
 // kernels replay the reference's own `multiply` / `shiftOmega` / `divZh` buffer semantics on the GPU.
 
-// Polynomial.degree (polynomial.js:212-226): *out = max(*out, highest index i > 0 with a[i] != 0).
-// One atomic per wave (wave-wide max first); *out is zeroed by the caller.
-__global__ void k_degree(uint32_t* __restrict__ out, const uint32_t* __restrict__ a, uint64_t len) {
+// Polynomial.degree (polynomial.js:212-226): *out = max(*out, highest index i > 0 with a[i] != 0);
+// *out is zeroed by the caller. A fixed grid of DEG_WAVES waves walks the vector downward from its
+// top end in 64-element chunks (wave w takes chunks w, w + DEG_WAVES, ...); a wave stops at its first
+// chunk with a nonzero element (everything it would read later is lower) or once its next chunk lies
+// below the maximum already found. A polynomial of full degree thus costs one chunk per wave and at
+// most one atomic each; the zero polynomial one streaming pass. (One atomic per wave over the whole
+// vector serialised on the one address: ~0.2 ms per 2^20 elements, ~1 ms per proof in
+// reference-quirks mode.)
+constexpr unsigned DEG_WAVES = 256;
+__global__ void __launch_bounds__(256) k_degree(uint32_t* __restrict__ out, const uint32_t* __restrict__ a, uint64_t len) {
   KGS_AUX_PRIO();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t d = 0;
-  if (i > 0 && i < len) {
-    const uint4 x = *(const uint4*)(a + 8 * i);
-    const uint4 y = *(const uint4*)(a + 8 * i + 4);
-    if (x.x | x.y | x.z | x.w | y.x | y.y | y.z | y.w) d = (uint32_t)i;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  for (uint64_t c = w;; c += DEG_WAVES) {
+    const uint64_t top = len - 1 - 64 * c;  // highest index of chunk c
+    if (64 * c + 1 >= len) break;           // (indices >= 1 only)
+    if (top <= __hip_atomic_load(out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    const uint64_t i = top - lane;
+    uint32_t d = 0;
+    if (lane <= top - 1) {  // i >= 1
+      const uint4 x = *(const uint4*)(a + 8 * i);
+      const uint4 y = *(const uint4*)(a + 8 * i + 4);
+      if (x.x | x.y | x.z | x.w | y.x | y.y | y.z | y.w) d = (uint32_t)i;
+    }
+    for (int o = 32; o > 0; o >>= 1) d = max(d, (uint32_t)__shfl_xor((int)d, o));
+    if (d) {
+      if (lane == 0) atomicMax(out, d);
+      break;
+    }
   }
-  for (int o = 32; o > 0; o >>= 1) d = max(d, (uint32_t)__shfl_xor((int)d, o));
-  if ((threadIdx.x & 63) == 0 && d) atomicMax(out, d);
 }
 void launch_degree(hipStream_t st, uint32_t* out, const uint32_t* a, uint64_t len) {
-  if (len > 1) hipLaunchKernelGGL(k_degree, dim3(nb(len)), dim3(256), 0, st, out, a, len);
+  if (len > 1) hipLaunchKernelGGL(k_degree, dim3(DEG_WAVES / 4), dim3(256), 0, st, out, a, len);
 }
 
 // The pointwise step of Polynomial.multiply / shiftOmega (polynomial.js:366-376, 378-393) on the

@@ -613,8 +613,6 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     throw KgsError(KGS_E_ARG, "a lookup needs both selectors (sel_t holds the multiplicities)");
   c.xs.reset();
   if (c.group) {
-    if (c.ref_quirks && in.kind != KGS_LOOKUP)
-      throw KgsError(KGS_E_ARG, "reference-quirks mode runs on the single-GPU prover only");
     prove_dist_group(c, in, com_out, ev_out);
     return;
   }
@@ -898,6 +896,12 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   fork_lanes(c);
   Commit cQ = commit_launch_split(c, Qc, qlen, qlen / 2, slot);
   slot += 2;
+  std::vector<const uint32_t*> qops = {polF, polT, Sc};
+  if (sel) {
+    qops.push_back(sFc);
+    qops.push_back(sTc);
+  }
+  const uint32_t* probe = c.ref_quirks && !lk ? ref_quirks_probe(c, n, qops, Qc, qlen) : nullptr;
   HC(hipMemcpyAsync(h_flags, flags, 64, hipMemcpyDeviceToHost, c.st));
   c.sync();
   // Reference-quirks mode (ref_quirks.cpp): where the reference's own quotient chain does not compute
@@ -906,13 +910,8 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   // on a zero quotient (divZh, after its divisibility check).
   const uint32_t* Fmut = nullptr;  // polF's buffer after the replay wrote into it (Q2), else nullptr
   bool replayed = false;
-  if (c.ref_quirks && !lk) {
-    std::vector<const uint32_t*> ops = {polF, polT, Sc};
-    if (sel) {
-      ops.push_back(sFc);
-      ops.push_back(sTc);
-    }
-    if (ref_quirks_needed(c, n, ops)) {
+  if (probe) {
+    if (ref_quirks_needed(probe, qops.size(), n)) {
       uint32_t* fm_out = nullptr;
       Qc = ref_quirks_quotient(c, gs, sel, lk, nbits, alpha, gamma, polF, polT, Sc, sFc, sTc, qlen, fm_out);
       Fmut = fm_out;
@@ -929,7 +928,7 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   }
   if (!replayed) {
     if (h_flags[1]) throw KgsError(KGS_E_NOT_DIVISIBLE, "Polynomial is not divisible");
-    if (c.ref_quirks && !lk && ref_quotient_is_zero(c, Qc, qlen)) throw KgsError(KGS_E_RANGE, "offset is out of bounds");
+    if (probe && ref_quotient_is_zero(probe)) throw KgsError(KGS_E_RANGE, "offset is out of bounds");
   }
   const int iQ = ci;
   commit_finish(c, cQ, com[ci++].data());
@@ -1108,7 +1107,10 @@ int kgs_ctx_create(int device, kgs_ctx_t** out) {
     // the second MSM lane and the copy stream are created on first use: contexts that never need
     // them keep one stream (several in-flight contexts share the device's few hardware queues)
     c->d_scal = c->buf("scalars", kgs_ctx::SCAL_BYTES);
-    if (const char* e = getenv("KGS_REFERENCE_QUIRKS")) c->ref_quirks = e[0] == '1';
+    // reference-identical behaviour on degenerate inputs by default (kgs.h); KGS_REFERENCE_QUIRKS=0
+    // selects the exact-math prover
+    c->ref_quirks = true;
+    if (const char* e = getenv("KGS_REFERENCE_QUIRKS")) c->ref_quirks = e[0] != '0';
     c->ensure_pin(8 << 20);
     *out = c;
     return KGS_OK;

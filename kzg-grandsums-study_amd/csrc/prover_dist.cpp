@@ -367,6 +367,47 @@ struct Dist {
   HostAllgather host_ag() {
     return [this](const void* s, void* rv, size_t b) { allgather(s, rv, b); };
   }
+  // Polynomial.degree (polynomial.js:212-226) of CYCLIC-sliced polynomials (rank r holds coefficients
+  // r + W j, j < Ml): the highest nonzero global index over all ranks, 0 for the zero polynomial
+  std::vector<uint64_t> degrees_cyc(const std::vector<const uint32_t*>& ops, uint64_t Ml) {
+    const size_t m = ops.size();
+    uint32_t* d = c.buf("d_qdeg", 4 * 16);
+    HC(hipMemsetAsync(d, 0, 4 * 16, c.st));
+    for (size_t i = 0; i < m; i++) launch_degree(c.st, d + i, ops[i], Ml);
+    check_launch();
+    uint8_t* h = c.pin(64 + 32 * m);
+    HC(hipMemcpyAsync(h, d, 64, hipMemcpyDeviceToHost, c.st));
+    for (size_t i = 0; i < m; i++) HC(hipMemcpyAsync(h + 64 + 32 * i, ops[i], 32, hipMemcpyDeviceToHost, c.st));
+    HC(hipStreamSynchronize(c.st));
+    std::vector<int64_t> mine(m);
+    for (size_t i = 0; i < m; i++) {
+      const uint32_t j = ((const uint32_t*)h)[i];
+      bool nz0 = false;
+      for (int b = 0; b < 32; b++) nz0 |= h[64 + 32 * i + b] != 0;
+      mine[i] = j ? (int64_t)r + (int64_t)W * j : (nz0 ? (int64_t)r : -1);
+    }
+    std::vector<int64_t> all(m * W);
+    allgather(mine.data(), all.data(), 8 * m);
+    std::vector<uint64_t> deg(m, 0);
+    for (size_t i = 0; i < m; i++)
+      for (int q = 0; q < W; q++) deg[i] = std::max<int64_t>((int64_t)deg[i], all[q * m + i]);
+    return deg;
+  }
+  // the full natural-order length-W*Ml vector of a CYCLIC-sliced polynomial, on this rank's device
+  // (reference-quirks replay only: a host all-gather of the slices)
+  uint32_t* gather_cyc(const uint32_t* sliceC, uint64_t Ml, const std::string& name) {
+    std::vector<uint8_t> mine((size_t)32 * Ml), all((size_t)32 * Ml * W), full((size_t)32 * Ml * W);
+    HC(hipMemcpyAsync(mine.data(), sliceC, mine.size(), hipMemcpyDeviceToHost, c.st));
+    HC(hipStreamSynchronize(c.st));
+    allgather(mine.data(), all.data(), mine.size());
+    for (int q = 0; q < W; q++)
+      for (uint64_t j = 0; j < Ml; j++)
+        memcpy(&full[(size_t)32 * (q + W * j)], &all[(size_t)32 * (q * Ml + j)], 32);
+    uint32_t* out = c.buf(name, full.size());
+    HC(hipMemcpyAsync(out, full.data(), full.size(), hipMemcpyHostToDevice, c.st));
+    HC(hipStreamSynchronize(c.st));
+    return out;
+  }
 };
 
 }  // namespace
@@ -623,7 +664,7 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
   tr.add_commitment(com[iS].data());
   const Fr alpha = tr.challenge();
   const uint32_t rot = (uint32_t)(cs >> nbits);
-  const uint64_t qlen = (!gs && !sel) ? n - 1 : 2 * n - 2;  // deg Q + 1 bound
+  uint64_t qlen = (!gs && !sel) ? n - 1 : 2 * n - 2;  // deg Q + 1 bound
   Fr gn = Fr::from_u64(5).pow_u64(n);
   // alpha_t: weight of the selT-binary term (none for a lookup, whose selT holds multiplicities)
   Fr qs[5] = {alpha, gamma, (gn - Fr::one()).inverse(), (gn.neg() - Fr::one()).inverse(), lk ? Fr::zero() : alpha};
@@ -652,11 +693,61 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
   launch_quotient_e(c.st, !gs, sel, Qe, cosS, cosF, cosT, cosSF, cosST, nxm1, d_qs, halo, Mc, W, r, (int)rot);
   check_launch();
   D.inv_e_to_cyc(Qc, Qe, lcs, true);
+  // Reference-quirks mode (ref_quirks.cpp; the single-GPU prover does the same in prover.cpp): where an
+  // operand of degree 1 <= d < n/2 makes the reference's multiply compute something else (Q1), its
+  // quotient chain is replayed on the gathered full operands, identically on every rank, and its Q —
+  // or its error — replaces ours; otherwise only its RangeError on a zero quotient (Q3) differs.
+  // Every decision here is made from all-gathered values, so all ranks throw the same error together.
+  bool replayed = false;
+  if (c.ref_quirks && !lk) {
+    std::vector<const uint32_t*> ops = {polF, polT, Sc};
+    if (sel) {
+      ops.push_back(sFc);
+      ops.push_back(sTc);
+    }
+    const std::vector<uint64_t> deg = D.degrees_cyc(ops, M);
+    bool need = false;
+    for (uint64_t d : deg) need |= d >= 1 && 2 * d < n;
+    if (need) {
+      c.dist_err_agreed = true;  // a failure of the replay is the same on every rank
+      const uint32_t* fF = D.gather_cyc(polF, M, "d_rq_F");
+      const uint32_t* fT = D.gather_cyc(polT, M, "d_rq_T");
+      const uint32_t* fS = D.gather_cyc(Sc, M, "d_rq_S");
+      const uint32_t* fSF = sel ? D.gather_cyc(sFc, M, "d_rq_SF") : nullptr;
+      const uint32_t* fST = sel ? D.gather_cyc(sTc, M, "d_rq_ST") : nullptr;
+      uint32_t* fmut = nullptr;
+      uint64_t qlen_ref = 0;
+      const uint32_t* Qref = ref_quirks_quotient(c, gs, sel, lk, nbits, alpha, gamma, fF, fT, fS, fSF, fST, qlen_ref, fmut);
+      if (fmut)
+        throw KgsError(KGS_E_ARG, "reference-quirks mode: the replay wrote into polF's buffer (Q2); not reproduced by a rank group");
+      if (qlen_ref > cs)
+        throw KgsError(KGS_E_ARG, "reference-quirks mode: the reference's Q has more coefficients than the group's coset layout");
+      // this rank's CYCLIC slice of the reference's Q (coefficients r + W j)
+      HC(hipMemsetAsync(Qc, 0, 32 * Mc, c.st));
+      const uint64_t cnt = qlen_ref > (uint64_t)r ? (qlen_ref - r + W - 1) / W : 0;
+      if (cnt) HC(hipMemcpy2DAsync(Qc, 32, Qref + 8 * r, (size_t)32 * W, 32, cnt, hipMemcpyDeviceToDevice, c.st));
+      qlen = qlen_ref;
+      replayed = true;
+      c.dist_err_agreed = false;
+    }
+  }
   Commit cQ = commit_cyc(Qc, qlen);
   uint32_t* h_flags = (uint32_t*)c.pin(64);
   HC(hipMemcpyAsync(h_flags, flags, 64, hipMemcpyDeviceToHost, c.st));
   c.sync();
-  if (D.gather_or(h_flags[1])) throw KgsError(KGS_E_NOT_DIVISIBLE, "Polynomial is not divisible");
+  if (!replayed) {
+    if (D.gather_or(h_flags[1])) throw KgsError(KGS_E_NOT_DIVISIBLE, "Polynomial is not divisible");
+    // Q3: the dividend of the reference's divZh has degree < n exactly when the quotient is zero
+    // (degree 0 over all ranks: only global coefficient 0, rank 0's first, can still be nonzero)
+    if (c.ref_quirks && !lk && D.degrees_cyc({Qc}, Mc)[0] == 0) {
+      uint8_t* h0 = c.pin(32);
+      HC(hipMemcpyAsync(h0, Qc, 32, hipMemcpyDeviceToHost, c.st));
+      HC(hipStreamSynchronize(c.st));
+      uint32_t nz = 0;
+      for (int b = 0; b < 32; b++) nz |= h0[b];
+      if (!D.gather_or(nz)) throw KgsError(KGS_E_RANGE, "offset is out of bounds");
+    }
+  }
   const int iQ = ci;
   commits_finish_with(c, {cQ}, {com[ci++].data()}, W, D.host_ag());
   lap(2);
@@ -827,11 +918,13 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
 // KGS_GROUP_TIMEOUT_S deadline of RcclGroup::wait).
 void prove_dist_group(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out) {
   c.xs.reset();
+  c.dist_err_agreed = false;
   dist_preconditions(c, in);
   try {
     prove_dist_impl(c, in, com_out, ev_out);
   } catch (const KgsError& e) {
-    if (e.code != KGS_E_NOT_WELL_CALC && e.code != KGS_E_NOT_DIVISIBLE && e.code != KGS_E_DOES_NOT_DIVIDE)
+    if (e.code != KGS_E_NOT_WELL_CALC && e.code != KGS_E_NOT_DIVISIBLE && e.code != KGS_E_DOES_NOT_DIVIDE &&
+        e.code != KGS_E_RANGE && !c.dist_err_agreed)
       c.group->abort();
     throw;
   } catch (...) {

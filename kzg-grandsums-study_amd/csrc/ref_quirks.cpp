@@ -218,35 +218,33 @@ struct Engine {
 
 }  // namespace
 
-// Which base operands have a degree the reference's multiply mis-sizes (1 <= d < n/2, all of them
-// length-n buffers): one degree kernel each, one sync.
-bool ref_quirks_needed(kgs_ctx& c, uint64_t n, const std::vector<const uint32_t*>& ops) {
+// The detection, enqueued on the main stream right after the quotient (no host round trip of its
+// own: the caller reads the pinned block after its next sync): the degrees of the base operands
+// (words 0..nops-1; length-n buffers), the degree of Q (word 8) and Q's coefficient 0 (words 16..23).
+uint32_t* ref_quirks_probe(kgs_ctx& c, uint64_t n, const std::vector<const uint32_t*>& ops, const uint32_t* Q,
+                           uint64_t qlen) {
   uint32_t* d = c.buf("refq_degs", 4 * 16);
   HC(hipMemsetAsync(d, 0, 4 * 16, c.st));
-  for (size_t i = 0; i < ops.size() && i < 16; i++) launch_degree(c.st, d + i, ops[i], n);
+  for (size_t i = 0; i < ops.size() && i < 8; i++) launch_degree(c.st, d + i, ops[i], n);
+  if (qlen) launch_degree(c.st, d + 8, Q, qlen);
   check_launch();
-  uint32_t* h = (uint32_t*)c.pin(64);
-  HC(hipMemcpyAsync(h, d, 4 * 16, hipMemcpyDeviceToHost, c.st));
-  HC(hipStreamSynchronize(c.st));
-  for (size_t i = 0; i < ops.size() && i < 16; i++)
-    if (h[i] >= 1 && 2ull * h[i] < n) return true;
+  uint32_t* h = (uint32_t*)c.pin(96);
+  HC(hipMemcpyAsync(h, d, 64, hipMemcpyDeviceToHost, c.st));
+  if (qlen) HC(hipMemcpyAsync(h + 16, Q, 32, hipMemcpyDeviceToHost, c.st));
+  else memset(h + 16, 0, 32);
+  return h;
+}
+// some base operand has a degree the reference's multiply mis-sizes (1 <= d < n/2)
+bool ref_quirks_needed(const uint32_t* probe, size_t nops, uint64_t n) {
+  for (size_t i = 0; i < nops && i < 8; i++)
+    if (probe[i] >= 1 && 2ull * probe[i] < n) return true;
   return false;
 }
-
 // Q3 on the fast path: the dividend has degree < n iff the (exact) quotient is the zero polynomial
-bool ref_quotient_is_zero(kgs_ctx& c, const uint32_t* Q, uint64_t qlen) {
-  if (qlen == 0) return true;
-  uint32_t* d = c.buf("refq_degs", 4 * 16);
-  HC(hipMemsetAsync(d, 0, 4, c.st));
-  launch_degree(c.st, d, Q, qlen);
-  check_launch();
-  uint32_t* h = (uint32_t*)c.pin(64);
-  HC(hipMemcpyAsync(h, d, 4, hipMemcpyDeviceToHost, c.st));
-  HC(hipMemcpyAsync(h + 8, Q, 32, hipMemcpyDeviceToHost, c.st));
-  HC(hipStreamSynchronize(c.st));
-  if (h[0]) return false;
+bool ref_quotient_is_zero(const uint32_t* probe) {
+  if (probe[8]) return false;
   for (int j = 0; j < 8; j++)
-    if (h[8 + j]) return false;
+    if (probe[16 + j]) return false;
   return true;
 }
 

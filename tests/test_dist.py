@@ -126,3 +126,65 @@ def test_gloo_sharded_msm(world):
     assert all(ok for _, ok, _ in res), res
     ranges = sorted(r[2] for r in res)
     assert ranges[0][0] == 0 and ranges[-1][1] == 37
+
+
+def _a2a_rank(rank, world, port, q):
+    try:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, common.ROOT)
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        K = common.load_pkg()
+        chunk = 96
+
+        def block(src, dst):
+            return bytes((31 * src + 7 * dst + i) % 256 for i in range(chunk))
+        send = b"".join(block(rank, j) for j in range(world))  # chunk j goes to rank j
+        out = K.torch_alltoall()(send, chunk)
+        ok = out == b"".join(block(s, rank) for s in range(world))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, ok, len(out)))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, False, repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_alltoall_transport(world):
+    """K.torch_alltoall (the host group's all-to-all callback, kgs_group_create_host_a2a): chunk j
+    of every rank's buffer reaches rank j, in source-rank order; a rank receives world chunks (one
+    vector), not world x its vector as through the all-gather-only transport"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_a2a_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
+    assert all(n == 96 * world for _, _, n in res)
+
+
+def test_dist_exchange_model():
+    """The all-to-alls of one distributed proof (csrc/prover_dist.cpp): a grand-sum
+    with k = 1 moves 12 vectors, 6 of length n and 6 of the 2n coset, i.e. 18 n-vector
+    equivalents, each sending L / W^2 elements to each of the W - 1 other ranks; selectors add two
+    of each; a vector adds two n-vectors per extra multiset; the unselected grand-product's coset
+    has n points. At n = 2^24 over 8 ranks that is 1.06 GB per rank (~1.1 GiB)."""
+    K = common.load_pkg()
+    n = 1 << 20
+    for W in (2, 4, 8, 16):
+        def unit(x):
+            return 32 * (W - 1) * x // (W * W)
+        m = K.dist_exchange_model(K.GRANDSUM, 20, 1, False, W)
+        assert m == {"alltoall_n": 12, "alltoall_bytes": unit(18 * n)}
+        m = K.dist_exchange_model(K.GRANDSUM, 20, 1, True, W)
+        assert m == {"alltoall_n": 16, "alltoall_bytes": unit(8 * n + 8 * 2 * n)}
+        m = K.dist_exchange_model(K.GRANDPRODUCT, 20, 1, False, W)
+        assert m == {"alltoall_n": 12, "alltoall_bytes": unit(12 * n)}
+        m = K.dist_exchange_model(K.GRANDSUM, 20, 3, False, W)
+        assert m == {"alltoall_n": 16, "alltoall_bytes": unit(22 * n)}
+        assert K.dist_exchange_model(K.LOOKUP, 20, 1, True, W) == K.dist_exchange_model(K.GRANDSUM, 20, 1, True, W)
+    assert K.dist_exchange_model(K.GRANDSUM, 24, 1, False, 8)["alltoall_bytes"] == 1056964608

@@ -230,17 +230,20 @@ def test_rccl_transport_world1(K):
     assert got[0] == want
 
 
-def _gloo_dist_rank(rank, world, port, ptau, q):
+def _gloo_dist_rank(rank, world, port, ptau, q, a2a):
     try:
         import torch.distributed as dist
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         K = common.load_pkg()
         ctx = K.Context(0)
         ctx.load_ptau(ptau, 10)
-        g = K.Group.host(world, K.torch_allgather())
+        g = K.Group.host(world, K.torch_allgather(), K.torch_alltoall() if a2a else None)
         ctx.set_group(g, rank)
         Fs, Ts, sF, sT = common.make_inputs(2718, 10, 2, True)
         coms, evs = ctx.prove(K.GRANDPRODUCT, 10, Fs, Ts, sF, sT, mont_out=False)[:2]
+        x = ctx.last_exchange()
+        if x["alltoall_bytes"] != K.dist_exchange_model(K.GRANDPRODUCT, 10, 2, True, world)["alltoall_bytes"]:
+            coms, evs = None, f"exchange bytes {x}"
         ctx.set_group(None)
         ctx.close()
         g.close()
@@ -251,8 +254,11 @@ def _gloo_dist_rank(rank, world, port, ptau, q):
         q.put((rank, None, repr(e)))
 
 
-def test_host_group_two_processes(K):
-    """one process per rank (as under torchrun) with the distributed prover over a gloo host group"""
+@pytest.mark.parametrize("a2a", [False, True])
+def test_host_group_two_processes(K, a2a):
+    """one process per rank (as under torchrun) with the distributed prover over a gloo host group:
+    all-gather only, and with the all-to-all callback (torch all_to_all_single: (W - 1) / W of a
+    vector leaves a rank per exchange)"""
     import multiprocessing as mp
     import socket
     ptau = gpu_ptau(K, 10)
@@ -264,7 +270,7 @@ def test_host_group_two_processes(K):
     s.close()
     mpc = mp.get_context("spawn")
     q = mpc.Queue()
-    procs = [mpc.Process(target=_gloo_dist_rank, args=(r, 2, port, ptau, q)) for r in range(2)]
+    procs = [mpc.Process(target=_gloo_dist_rank, args=(r, 2, port, ptau, q, a2a)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=600) for _ in range(2)]
@@ -273,6 +279,31 @@ def test_host_group_two_processes(K):
     for rank, coms, evs in res:
         assert coms is not None, evs
         assert (coms, evs) == want, rank
+
+
+@pytest.mark.parametrize("world,kind,nbits,npols,sel", [(2, 0, 10, 1, False), (4, 1, 10, 2, True), (8, 1, 9, 1, False)])
+def test_exchange_stats_match_the_model(K, world, kind, nbits, npols, sel):
+    """kgs_last_exchange on every rank: the all-to-all count and the bytes that left the rank are
+    those of K.dist_exchange_model (the DESIGN.md §6 plan the bench's exchange fields are read
+    against); the spans are positive; a single-GPU proof afterwards reports zeros"""
+    ptau = gpu_ptau(K, 12)
+    Fs, Ts, sF, sT = common.make_inputs(99, nbits, npols, sel)
+    g = K.Group.local(world)
+    ctxs = [K.Context(0) for _ in range(world)]
+    for c in ctxs:
+        c.load_ptau(ptau, nbits)
+    got, err = run_group(K, g, world, ptau, kind, nbits, Fs, Ts, sF, sT, ctxs=ctxs, keep=True)
+    assert not any(err), err
+    model = K.dist_exchange_model(kind, nbits, npols, sel, world)
+    for c in ctxs:
+        x = c.last_exchange()
+        assert x["alltoall_n"] == model["alltoall_n"] and x["alltoall_bytes"] == model["alltoall_bytes"], (x, model)
+        assert x["alltoall_ms"] > 0 and x["allgather_n"] > 0 and x["allgather_bytes"] > 0
+    ctxs[0].prove(kind, nbits, Fs, Ts, sF, sT, mont_out=False)
+    assert ctxs[0].last_exchange()["alltoall_n"] == 0
+    for c in ctxs:
+        c.close()
+    g.close()
 
 
 def test_dist_matches_oracle_small(K):

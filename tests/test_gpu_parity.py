@@ -250,27 +250,32 @@ def test_error_paths(K):
         K.grandsum_prover(path, K.Evaluations(big[0]), K.Evaluations(bigT[0]))
 
 
-def test_trivial_identity_multiset(K):
+def test_trivial_identity_multiset(K, monkeypatch):
     """F == T: S == 0 (grand-sum) / Z == 1; commitments of zero polynomials are infinity. The quotient
     is zero, on which the reference's divZh throws V8's RangeError (oracle quirk Q3,
-    tests/test_gpu_quirks.py): the default mode proves it with the exact values (oracle quirks=False)."""
+    tests/test_gpu_quirks.py): so does the default (reference-identical) mode; the exact-math mode
+    (KGS_REFERENCE_QUIRKS=0) proves it with the exact values (oracle quirks=False)."""
     from oracle import poly as OP
     Fs, _, _, _ = common.make_inputs(8, 3, 1, False)
     srs = P.SRS(common.oracle_ptau(9), common.tau())
     for kind, fn in (("grandsum", K.grandsum_prover), ("grandproduct", K.grandproduct_prover)):
+        monkeypatch.delenv("KGS_REFERENCE_QUIRKS", raising=False)
+        with pytest.raises(K.RangeError, match="offset is out of bounds"):
+            fn(common.oracle_ptau(9), K.Evaluations(Fs[0]), K.Evaluations(Fs[0]))
+        with pytest.raises(OP.JSRangeError, match="offset is out of bounds"):
+            P.prove(kind, srs, P.EvalBuffer(Fs[0]), P.EvalBuffer(Fs[0]))
+        monkeypatch.setenv("KGS_REFERENCE_QUIRKS", "0")
         got = fn(common.oracle_ptau(9), K.Evaluations(Fs[0]), K.Evaluations(Fs[0]))
         exp = P.prove(kind, srs, P.EvalBuffer(Fs[0]), P.EvalBuffer(Fs[0]), quirks=False)
         assert got == exp
-        with pytest.raises(OP.JSRangeError, match="offset is out of bounds"):
-            P.prove(kind, srs, P.EvalBuffer(Fs[0]), P.EvalBuffer(Fs[0]))
 
 
-def test_all_zero_selectors(K):
+def test_all_zero_selectors(K, monkeypatch):
     """selF = selT = 0 with F, T unrelated: trivially satisfied — the reference warns "The selection
     buffers are all zeros" (src/grandsum/mset_eq_kzg_prover.js:66-68); S = 0 and Z = 1, so several
     commitments are of constant polynomials and the quotient is zero, on which the reference's divZh
-    then throws V8's RangeError (oracle quirk Q3). Default mode: byte-exact vs the oracle's exact values
-    (quirks=False), verified."""
+    then throws V8's RangeError (oracle quirk Q3) — and so does the default mode. Exact-math mode
+    (KGS_REFERENCE_QUIRKS=0): byte-exact vs the oracle's exact values (quirks=False), verified."""
     from oracle import poly as OP
     ptau = common.oracle_ptau(9)
     srs = P.SRS(ptau, common.tau())
@@ -279,6 +284,11 @@ def test_all_zero_selectors(K):
     zero = common.mont_bytes([0] * 16)
     for kind, fn, vf in (("grandsum", K.grandsum_prover, K.grandsum_verifier),
                          ("grandproduct", K.grandproduct_prover, K.grandproduct_verifier)):
+        monkeypatch.delenv("KGS_REFERENCE_QUIRKS", raising=False)
+        with pytest.raises(K.RangeError, match="offset is out of bounds"):
+            fn(ptau, [K.Evaluations(x) for x in Fs], [K.Evaluations(x) for x in Ts], K.Evaluations(zero),
+               K.Evaluations(zero))
+        monkeypatch.setenv("KGS_REFERENCE_QUIRKS", "0")
         got = fn(ptau, [K.Evaluations(x) for x in Fs], [K.Evaluations(x) for x in Ts],
                  K.Evaluations(zero), K.Evaluations(zero))
         exp = P.prove(kind, srs, [P.EvalBuffer(x) for x in Fs], [P.EvalBuffer(x) for x in Ts],

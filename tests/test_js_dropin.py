@@ -482,9 +482,10 @@ def test_js_rewritten_ptau_is_reread(tmp_path):
 @pytest.mark.gpu
 def test_js_reference_quirks(tmp_path):
     """Degenerate valid multisets through the JS drop-in (DESIGN.md §4 "Reference quirks",
-    tests/test_gpu_quirks.py): by default the module proves them (byte-identical to the oracle's
-    exact-value semantics, verified by the drop-in verifier); with KGS_REFERENCE_QUIRKS=1 it throws what
-    the reference throws — an Error with its message, or V8's RangeError for a zero quotient."""
+    tests/test_gpu_quirks.py): by default (and with KGS_REFERENCE_QUIRKS=1) it throws what the reference
+    throws — an Error with its message, or V8's RangeError for a zero quotient; with
+    KGS_REFERENCE_QUIRKS=0 (exact-math mode) it proves them (byte-identical to the oracle's exact-value
+    semantics, verified by the drop-in verifier)."""
     import test_gpu_quirks as Q
     ptau = common.oracle_ptau(9)
     srs = P.SRS(ptau, common.tau())
@@ -500,10 +501,11 @@ def test_js_reference_quirks(tmp_path):
         ref.append(Q.oracle_outcome(kind, ptau, Fs, Ts, sF, sT, quirks=True))
     spec = tmp_path / "spec.json"
     spec.write_text(json.dumps({"ptau": ptau, "cases": cases, "verify": True}))
-    for quirks in (False, True):
+    for mode in ("0", None, "1"):
+        quirks = mode != "0"
         env = {k: v for k, v in os.environ.items() if k != "KGS_REFERENCE_QUIRKS"}
-        if quirks:
-            env["KGS_REFERENCE_QUIRKS"] = "1"
+        if mode is not None:
+            env["KGS_REFERENCE_QUIRKS"] = mode
         out = json.loads(subprocess.check_output([NODE, os.path.join(JS, "test", "prove_from_json.js"), str(spec)],
                                                  timeout=600, env=env))
         for got, ex, rf in zip(out["proofs"], exact, ref):
