@@ -1551,9 +1551,12 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   using hclk = std::chrono::steady_clock;
   const auto h0 = hclk::now();
   // each vector in pieces: the host copy of piece p + 1 into the pinned slot runs while piece p is
-  // DMA'd, so a vector's DMA ends one piece after its host copy instead of a whole vector after
-  const size_t piece = (size_t)8 << 20;
+  // DMA'd, so a vector's DMA ends one piece after its host copy instead of a whole vector after.
+  // Vector 0 (F_0, whose transform starts round 1) in 2 MiB pieces, so that its first DMA starts
+  // ~0.03 ms into the call and its last ends ~0.04 ms after its copy; the others in 8 MiB pieces
+  // (fewer DMA submissions on the feeder thread)
   auto feed = [&](size_t v, hipStream_t st) {
+    const size_t piece = (size_t)(v == 0 ? 2 : 8) << 20;
     for (size_t o = 0; o < E; o += piece) {
       const size_t len = std::min(piece, E - o);
       par_copy({{in_jobs[v].dst + o, in_jobs[v].src + o, len}});

@@ -56,6 +56,32 @@ CLASSES = [("v_mad_u64_u32", "mad 32x32+64 (partial products)"),
            ("", "other")]
 
 
+# measured issue cost per wave64 instruction, SIMD cycles at the nominal clock
+# (profiles/ubench/issue_rates2.hip -> profiles/ubench/issue_rates2_r03.txt); VOP2 32-bit ops ~2.3-2.8,
+# every VOP3 / 64-bit op ~4.2-4.4 (v_cndmask_b32's 22.9 there is its benchmark's VCC dependency, not
+# the op: priced as a VOP2 op)
+ISSUE = {"v_mad_u64_u32": 4.16, "v_mul_lo_u32": 4.28, "v_and_b32_e32": 2.49, "v_lshrrev_b64": 4.16,
+         "v_lshl_add_u64": 4.40, "v_ashrrev_i64": 4.16, "v_sub_u32_e32": 2.47, "v_add_u32_e32": 2.82,
+         "v_alignbit_b32": 4.16, "v_lshrrev_b32_e32": 2.28, "v_lshlrev_b32_e32": 2.28, "v_add3_u32": 4.20,
+         "v_lshl_add_u32": 4.18, "v_or3_b32": 4.17, "v_or_b32_e32": 2.47, "v_cndmask_b32_e32": 2.49,
+         "v_mov_b32_e32": 2.24, "v_bfe_u32": 4.15, "v_lshl_or_b32": 4.17}
+
+
+def issue_cycles(ops):
+    """(total SIMD cycles, cycles by opcode) of a straight-line instruction list: VALU at the measured
+    per-opcode cost (unlisted VOP3 forms 4.2, unlisted 32-bit VOP2 forms 2.4); scalar / memory not
+    counted (they issue on other ports)"""
+    by = collections.Counter()
+    for op in ops:
+        if not op.startswith("v_"):
+            continue
+        c = ISSUE.get(op)
+        if c is None:
+            c = 2.4 if op.endswith("_e32") else 4.2
+        by[op] += c
+    return sum(by.values()), by
+
+
 def classify(op):
     for pre, name in CLASSES:
         if op.startswith(pre):
@@ -96,6 +122,13 @@ def main():
               file=out)
         print(f"   per 254-bit product (10 product-equivalents: 6 mul + 2 sqr + 1 lazily reduced double product"
               f" counted as 1.5 + ...): mads {mads} = 6 x 162 + 2 x 126 + 243", file=out)
+        tot, by = issue_cycles(hot)
+        print(f"\n== issue cycles of the common path per bucket entry (measured per-opcode costs): {tot:.0f} SIMD cycles",
+              file=out)
+        for op, cyc in by.most_common(12):
+            print(f"   {op:22s} {cyc:7.0f}  ({100 * cyc / tot:4.1f} %)", file=out)
+        print(f"   non-mad: {tot - by['v_mad_u64_u32']:.0f} cycles ({100 * (tot - by['v_mad_u64_u32']) / tot:.1f} %)",
+              file=out)
     finally:
         shutil.rmtree(tmp)
 
