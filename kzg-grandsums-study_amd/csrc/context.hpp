@@ -109,11 +109,18 @@ struct DomainTables {
   int device = 0, logM = -1;
   uint32_t* mem = nullptr;
   uint32_t *tw_fwd = nullptr, *tw_inv = nullptr, *coset_pow = nullptr, *coset_ipow = nullptr, *invm = nullptr;
+  // the stage twiddles again as 9 x 29-bit limbs of w * 2^261 (10 words each, fr29.hpp): the LDS NTT
+  // passes' products (ntt_register_tw29 maps tw_fwd / tw_inv to these)
+  uint32_t* mem29 = nullptr;
+  uint32_t *tw29_fwd = nullptr, *tw29_inv = nullptr;
   ~DomainTables() {
-    if (mem) {
-      hipSetDevice(device);
-      hipFree(mem);
+    hipSetDevice(device);
+    if (mem29) {
+      ntt_unregister_tw29(tw_fwd);
+      ntt_unregister_tw29(tw_inv);
+      hipFree(mem29);
     }
+    if (mem) hipFree(mem);
   }
 };
 

@@ -59,6 +59,13 @@ struct MsmWork {
 // NTT LDS passes built for three waves per SIMD (co-resident with two accumulate waves: proofs in
 // flight) or two (fastest alone) for the calling thread's later launches; returns the previous setting
 bool ntt_set_coresident(bool on);
+constexpr int TW29_WORDS = 10;  // words per 29-bit twiddle record (fr29.hpp W29_WORDS)
+// the 29-bit twiddle table (fr29.hpp, k_tw29 records) of an 8 x 32 stage table: the LDS passes of
+// ntt_dif / ntt_dit look up the table they were given and multiply by its 29-bit twin when registered
+void ntt_register_tw29(const uint32_t* tw, const uint32_t* tw29);
+void ntt_unregister_tw29(const uint32_t* tw);
+// out[i] = the k_tw29 record of in[i] (8 x 32 Montgomery words), i < count
+void launch_tw29(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t count);
 void ntt_dif(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t in_len, int logm, const uint32_t* pre,
              const uint32_t* tw, int logM);
 void ntt_dit(hipStream_t st, uint32_t* out, const uint32_t* in, int in_bitrev, int logm, const uint32_t* tw, int logM,

@@ -19,7 +19,12 @@
 // (coalesced: consecutive lanes have consecutive t) instead of a strided walk through w_M^j.
 #include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <type_traits>
+#include <utility>
 
+#include "fr29.hpp"
 #include "kernels.hpp"
 
 namespace kgs {
@@ -270,6 +275,37 @@ __device__ __forceinline__ void ntt_store(const ntt_io& io, uint64_t idx, fr y) 
   canon_out(y).store(io.data + 8 * idx);
 }
 
+// Twiddles of the LDS passes: `fr` (8 x 32-bit words, fr::mul_nored_x2) or, since round 5, `W29`
+// (the 29-bit records of the domain's twin tables, fr29.hpp mul29: 9 independent column chains per
+// product instead of one; the two products of a pair are independent, so the compiler interleaves
+// them itself). Both give a product in [0, 2p) of the same residue: the canonical pass outputs are
+// bit-identical.
+template <typename TW>
+__device__ __forceinline__ TW tw_load(const uint32_t* tw, uint32_t idx);
+template <>
+__device__ __forceinline__ fr tw_load<fr>(const uint32_t* tw, uint32_t idx) { return fr::load(tw + 8 * idx); }
+template <>
+__device__ __forceinline__ W29 tw_load<W29>(const uint32_t* tw, uint32_t idx) {
+  return w29_load(tw + TW29_WORDS * idx);
+}
+__device__ __forceinline__ void mul_tw_x2(const fr& a, const fr& wa, const fr& b, const fr& wb, fr& ra, fr& rb) {
+  fr::mul_nored_x2(a, wa, b, wb, ra, rb);
+}
+__device__ __forceinline__ void mul_tw_x2(const fr& a, const W29& wa, const fr& b, const W29& wb, fr& ra, fr& rb) {
+  ra = mul29(a, wa);
+  rb = mul29(b, wb);
+}
+
+// for (I = 0; I < N; I++) f(integral_constant<I>) with every iteration expanded at compile time
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 // butterfly groups of lds_round: (r, r + dist) for the given register indices
 __device__ __forceinline__ void bfly_pair_triv(fr* x, int r0, int r1, int dist) {  // w = 1 for both
   const fr a0 = x[r0], b0 = x[r0 + dist], a1 = x[r1], b1 = x[r1 + dist];
@@ -278,11 +314,11 @@ __device__ __forceinline__ void bfly_pair_triv(fr* x, int r0, int r1, int dist) 
   x[r1] = fr::add_lazy(a1, b1);
   x[r1 + dist] = fr::sub_lazy(a1, b1);
 }
-template <bool DIT>
-__device__ __forceinline__ void bfly_pair_x2(fr* x, int r0, int r1, int dist, const fr& w0, const fr& w1) {
+template <bool DIT, typename TW>
+__device__ __forceinline__ void bfly_pair_x2(fr* x, int r0, int r1, int dist, const TW& w0, const TW& w1) {
   if (DIT) {
     fr b0, b1;
-    fr::mul_nored_x2(x[r0 + dist], w0, x[r1 + dist], w1, b0, b1);
+    mul_tw_x2(x[r0 + dist], w0, x[r1 + dist], w1, b0, b1);
     const fr a0 = x[r0], a1 = x[r1];
     x[r0] = fr::add_lazy(a0, b0);
     x[r0 + dist] = fr::sub_lazy(a0, b0);
@@ -292,12 +328,12 @@ __device__ __forceinline__ void bfly_pair_x2(fr* x, int r0, int r1, int dist, co
     const fr d0 = fr::sub_2p(x[r0], x[r0 + dist]), d1 = fr::sub_2p(x[r1], x[r1 + dist]);
     x[r0] = fr::add_lazy(x[r0], x[r0 + dist]);
     x[r1] = fr::add_lazy(x[r1], x[r1 + dist]);
-    fr::mul_nored_x2(d0, w0, d1, w1, x[r0 + dist], x[r1 + dist]);
+    mul_tw_x2(d0, w0, d1, w1, x[r0 + dist], x[r1 + dist]);
   }
 }
 // one register round of R stages of a pass on the 2^R elements j = jb + js * r (r < 2^R) of column
 // col: stage k of the round is pass stage kp0 + k; DIF pairs (r, r + 2^(R-1-k)), DIT (r, r + 2^k)
-template <int R, bool DIT, bool GIN, bool GOUT, bool PF>
+template <int R, bool DIT, bool GIN, bool GOUT, bool PF, typename TW>
 __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restrict__ tw, const ntt_io& io, uint32_t cl,
                                           uint32_t col, uint32_t jb, uint32_t js, int K, int logd, int lb, int kp0) {
   fr x[1 << R];
@@ -353,19 +389,22 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
     }
     // PF: the next step's twiddles loaded before this step's butterflies (the 2-wave build); the
     // 3-wave build (<= 168 VGPRs) loads each step's own twiddles, which saves their registers
-    fr wa, wb;
+    TW wa, wb;
     if (PF) {
-      wa = fr::load(tw + 8 * tw0[0]);
-      wb = fr::load(tw + 8 * tw1[0]);
+      wa = tw_load<TW>(tw, tw0[0]);
+      wb = tw_load<TW>(tw, tw1[0]);
     }
-#pragma unroll
-    for (int st = 0; st < NSTEP; st++) {
-      const int k = st / half, qa = st % half;
-      const int dist = DIT ? 1 << k : 1 << (R - 1 - k);
-      const int r0 = ((qa / dist) * 2 * dist) + (qa % dist), r1 = (((qa + half) / dist) * 2 * dist) + ((qa + half) % dist);
+    // a compile-time loop: with the larger 29-bit products LLVM stopped unrolling the step loop and
+    // indexed x[] dynamically, i.e. through scratch memory; here every step's register indices are
+    // constants whatever the body's size
+    static_for<NSTEP>([&](auto stc) {
+      constexpr int st = decltype(stc)::value;
+      constexpr int k = st / half, qa = st % half;
+      constexpr int dist = DIT ? 1 << k : 1 << (R - 1 - k);
+      constexpr int r0 = ((qa / dist) * 2 * dist) + (qa % dist), r1 = (((qa + half) / dist) * 2 * dist) + ((qa + half) % dist);
       if (PF) {
-        const int nx = st + 1 < NSTEP ? st + 1 : st;  // the last step reloads its own twiddles (unused)
-        const fr na = fr::load(tw + 8 * tw0[nx]), nb = fr::load(tw + 8 * tw1[nx]);
+        constexpr int nx = st + 1 < NSTEP ? st + 1 : st;  // the last step reloads its own twiddles (unused)
+        const TW na = tw_load<TW>(tw, tw0[nx]), nb = tw_load<TW>(tw, tw1[nx]);
         if (triv[st])
           bfly_pair_triv(x, r0, r1, dist);
         else
@@ -375,12 +414,13 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
       } else if (triv[st]) {
         bfly_pair_triv(x, r0, r1, dist);
       } else {
-        bfly_pair_x2<DIT>(x, r0, r1, dist, fr::load(tw + 8 * tw0[st]), fr::load(tw + 8 * tw1[st]));
+        bfly_pair_x2<DIT>(x, r0, r1, dist, tw_load<TW>(tw, tw0[st]), tw_load<TW>(tw, tw1[st]));
       }
-    }
+    });
   } else
 #endif
   {
+    static_assert(sizeof(TW) == sizeof(fr), "the single-butterfly path reads 8 x 32-bit twiddles only");
 #pragma unroll
     for (int k = 0; k < R; k++) {
       const int kp = kp0 + k;                                 // stage within the pass
@@ -430,14 +470,14 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
 // tile (a thread holds the 2^R elements that differ in those bits, the other K - R bits fixed).
 // DIF rounds run from the top j-bits down, DIT rounds from bit 0 up; kp0 = the round's first stage
 // within the pass.
-template <int R, bool DIT, bool GIN, bool GOUT, bool PF>
+template <int R, bool DIT, bool GIN, bool GOUT, bool PF, typename TW>
 __device__ __forceinline__ void lds_round_all(uint32_t* lds, const uint32_t* __restrict__ tw, const ntt_io& io,
                                               uint32_t col0, int K, int logd, int lblog, int b0) {
   const int kp0 = DIT ? b0 : K - b0 - R;
   for (uint32_t g = threadIdx.x; g < (LDS_ELEMS >> R); g += LDS_NT) {
     const uint32_t cl = g & ((1u << lblog) - 1), jq = g >> lblog;
     const uint32_t jb = (jq & ((1u << b0) - 1)) | ((jq >> b0) << (b0 + R));
-    lds_round<R, DIT, GIN, GOUT, PF>(lds, tw, io, cl, col0 + cl, jb, 1u << b0, K, logd, 1 << lblog, kp0);
+    lds_round<R, DIT, GIN, GOUT, PF, TW>(lds, tw, io, cl, col0 + cl, jb, 1u << b0, K, logd, 1 << lblog, kp0);
   }
 }
 
@@ -456,9 +496,11 @@ __device__ __forceinline__ void lds_round_all(uint32_t* lds, const uint32_t* __r
 #ifndef KGS_NTT_PF3
 #define KGS_NTT_PF3 0
 #endif
-template <int K1, int K2, int K3, bool DIT, bool DIRECT, int WV>
+// T29: the twiddle products in 9 x 29-bit limbs (tw = the domain's 29-bit twin table, fr29.hpp)
+template <int K1, int K2, int K3, bool DIT, bool DIRECT, int WV, bool T29>
 __global__ void __launch_bounds__(LDS_NT) __attribute__((amdgpu_waves_per_eu(WV, WV)))
 k_ntt_lds_pass(ntt_io io, const uint32_t* __restrict__ tw, int s0) {
+  using TW = typename std::conditional<T29, W29, fr>::type;
   KGS_AUX_PRIO();
   constexpr int K = K1 + K2 + K3;
   constexpr int LBLOG = NTT_ELOG - K;
@@ -485,14 +527,14 @@ k_ntt_lds_pass(ntt_io io, const uint32_t* __restrict__ tw, int s0) {
   }
   // DIF: bits [K-K1, K), [K-K1-K2, K-K1), [0, K3); DIT: [0, K1), [K1, K1+K2), [K1+K2, K)
   constexpr bool PF = WV < 3 || KGS_NTT_PF3;
-  lds_round_all<K1, DIT, DIRECT, false, PF>(lds, tw, io, col0, K, logd, LBLOG, DIT ? 0 : K - K1);
+  lds_round_all<K1, DIT, DIRECT, false, PF, TW>(lds, tw, io, col0, K, logd, LBLOG, DIT ? 0 : K - K1);
   __syncthreads();
   if constexpr (K3 > 0) {
-    lds_round_all<K2, DIT, false, false, PF>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 : K3);
+    lds_round_all<K2, DIT, false, false, PF, TW>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 : K3);
     __syncthreads();
-    lds_round_all<K3, DIT, false, DIRECT, PF>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 + K2 : 0);
+    lds_round_all<K3, DIT, false, DIRECT, PF, TW>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 + K2 : 0);
   } else {
-    lds_round_all<K2, DIT, false, DIRECT, PF>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 : 0);
+    lds_round_all<K2, DIT, false, DIRECT, PF, TW>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 : 0);
   }
   if (!DIRECT) {  // store (address order)
     __syncthreads();
@@ -506,6 +548,49 @@ k_ntt_lds_pass(ntt_io io, const uint32_t* __restrict__ tw, int s0) {
 
 // the calling thread's pass build (ntt_set_coresident; per thread: contexts prove on their callers' threads)
 thread_local bool g_ntt_coresident = false;
+
+// 8 x 32 stage table -> its registered 29-bit twin (the shared domain tables register theirs when
+// built, unregister when freed); KGS_NTT_T29=0 keeps the 8 x 32 products (A/B)
+static std::mutex g_tw29_mu;
+static std::map<const uint32_t*, const uint32_t*> g_tw29;
+void ntt_register_tw29(const uint32_t* tw, const uint32_t* tw29) {
+  std::lock_guard<std::mutex> lk(g_tw29_mu);
+  g_tw29[tw] = tw29;
+}
+void ntt_unregister_tw29(const uint32_t* tw) {
+  std::lock_guard<std::mutex> lk(g_tw29_mu);
+  g_tw29.erase(tw);
+}
+static const uint32_t* tw29_of(const uint32_t* tw) {
+  static const bool off = [] {
+    const char* e = getenv("KGS_NTT_T29");
+    return e && e[0] == '0';
+  }();
+  if (off) return nullptr;
+  std::lock_guard<std::mutex> lk(g_tw29_mu);
+  auto it = g_tw29.find(tw);
+  return it == g_tw29.end() ? nullptr : it->second;
+}
+
+// the 29-bit record of a stage twiddle (fr29.hpp): w * 2^261 mod p (= its Montgomery form times the
+// Montgomery form of 32), canonical, in 9 limbs + a zero pad word
+__global__ void k_tw29(uint32_t* __restrict__ out, const uint32_t* __restrict__ in, uint64_t count) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  fr c;
+#pragma unroll
+  for (int k = 0; k < 8; k++) c.v[k] = r29::C32[k];
+  const fr x = fr::load(in + 8 * i) * c;
+  uint32_t l[9];
+  unpack29(x, l);
+  uint32_t* o = out + (uint64_t)TW29_WORDS * i;
+#pragma unroll
+  for (int k = 0; k < 9; k++) o[k] = l[k];
+  o[9] = 0;
+}
+void launch_tw29(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t count) {
+  hipLaunchKernelGGL(k_tw29, dim3(nblocks(count)), dim3(256), 0, st, out, in, count);
+}
 
 #ifndef KGS_NO_NTT_LDS
 // LDS passes need m >= the tile (2^NTT_ELOG elements)
@@ -539,13 +624,21 @@ static void launch_lds_pass(hipStream_t st, int K, bool dit, uint32_t* data, con
   const int logd = dit ? s0 : logm - s0 - K;
   static const bool staged = getenv("KGS_NTT_STAGED") != nullptr;  // A/B: every pass staged through LDS
   const bool direct = logd >= NTT_ELOG - K && !staged;
-#define KGS_LDS_LAUNCH(A, B, C, D, E)                                                                          \
+  const uint32_t* tw29 = tw29_of(tw);  // the 29-bit twin table, if the domain registered one
+#define KGS_LDS_LAUNCH2(A, B, C, D, E, T, TWP)                                                                 \
   do {                                                                                                         \
     if (g_ntt_coresident)                                                                                      \
-      hipLaunchKernelGGL((k_ntt_lds_pass<A, B, C, D, E, 3>), dim3(blocks), dim3(LDS_NT), LDS_ELEMS * 32, st, io, \
-                         tw, s0);                                                                              \
+      hipLaunchKernelGGL((k_ntt_lds_pass<A, B, C, D, E, 3, T>), dim3(blocks), dim3(LDS_NT), LDS_ELEMS * 32, st, \
+                         io, TWP, s0);                                                                         \
     else                                                                                                       \
-      hipLaunchKernelGGL((k_ntt_lds_pass<A, B, C, D, E, 2>), dim3(blocks), dim3(LDS_NT), 0, st, io, tw, s0);   \
+      hipLaunchKernelGGL((k_ntt_lds_pass<A, B, C, D, E, 2, T>), dim3(blocks), dim3(LDS_NT), 0, st, io, TWP, s0); \
+  } while (0)
+#define KGS_LDS_LAUNCH(A, B, C, D, E)             \
+  do {                                            \
+    if (tw29)                                     \
+      KGS_LDS_LAUNCH2(A, B, C, D, E, true, tw29); \
+    else                                          \
+      KGS_LDS_LAUNCH2(A, B, C, D, E, false, tw);  \
   } while (0)
 #define KGS_LDS_BY_K(D, E)                          \
   switch (K) {                                      \
@@ -571,6 +664,7 @@ static void launch_lds_pass(hipStream_t st, int K, bool dit, uint32_t* data, con
   }
 #undef KGS_LDS_BY_K
 #undef KGS_LDS_LAUNCH
+#undef KGS_LDS_LAUNCH2
 }
 #endif
 

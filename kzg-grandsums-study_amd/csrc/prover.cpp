@@ -120,6 +120,12 @@ void ensure_domain(kgs_ctx& c, int logM) {
   }
   launch_powers(c.st, d->coset_pow, M, dc + 16 * logM, nullptr);
   launch_powers(c.st, d->coset_ipow, M, dc + 16 * logM + 8, nullptr);
+  // 29-bit twins of the stage tables for the LDS passes' products (fr29.hpp)
+  HC(dev_malloc((void**)&d->mem29, (size_t)4 * 2 * TW29_WORDS * M));
+  d->tw29_fwd = d->mem29;
+  d->tw29_inv = d->mem29 + (size_t)TW29_WORDS * M;
+  launch_tw29(c.st, d->tw29_fwd, d->tw_fwd, M);
+  launch_tw29(c.st, d->tw29_inv, d->tw_inv, M);
   std::vector<Fr> im(logM + 1);
   for (int l = 0; l <= logM; l++) im[l] = Fr::from_u64(1ull << l).inverse();
   uint8_t* h = c.pin(32 * (logM + 1));
@@ -129,6 +135,8 @@ void ensure_domain(kgs_ctx& c, int logM) {
   c.sync();  // built: publish
   c.h_pin_off = pin_mark;
   c.d_scal_off = scal_mark;
+  ntt_register_tw29(d->tw_fwd, d->tw29_fwd);
+  ntt_register_tw29(d->tw_inv, d->tw29_inv);
   d->logM = logM;
   g_dom_reg.erase(std::remove_if(g_dom_reg.begin(), g_dom_reg.end(), [](auto& w) { return w.expired(); }),
                   g_dom_reg.end());
