@@ -109,15 +109,14 @@ struct DomainTables {
   int device = 0, logM = -1;
   uint32_t* mem = nullptr;
   uint32_t *tw_fwd = nullptr, *tw_inv = nullptr, *coset_pow = nullptr, *coset_ipow = nullptr, *invm = nullptr;
-  // the stage twiddles again as 9 x 29-bit limbs of w * 2^261 (10 words each, fr29.hpp): the LDS NTT
-  // passes' products (ntt_register_tw29 maps tw_fwd / tw_inv to these)
+  // every table of `mem` again as 9 x 29-bit limbs of x * 2^261 (10 words per element, fr29.hpp): the
+  // LDS NTT passes' twiddle and scaling products (ntt_register_tw29 maps a pointer into `mem` to its
+  // record here)
   uint32_t* mem29 = nullptr;
-  uint32_t *tw29_fwd = nullptr, *tw29_inv = nullptr;
   ~DomainTables() {
     hipSetDevice(device);
     if (mem29) {
-      ntt_unregister_tw29(tw_fwd);
-      ntt_unregister_tw29(tw_inv);
+      ntt_unregister_tw29(mem);
       hipFree(mem29);
     }
     if (mem) hipFree(mem);
@@ -431,6 +430,7 @@ struct EvalJob {
   Fr x;
 };
 uint32_t* xpowers(kgs_ctx& c, const Fr& x);
+void fr29_record(const Fr& x, Fr out[2]);
 EvalJob eval_launch(kgs_ctx& c, const std::vector<const uint32_t*>& src, const std::vector<uint64_t>& len, const Fr& x,
                     int slot);
 std::vector<Fr> eval_finish(const EvalJob& j);

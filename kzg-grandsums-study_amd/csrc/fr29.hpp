@@ -29,6 +29,9 @@ constexpr int W29_WORDS = 10;            // twiddle record: 9 limbs + 1 pad (ker
 // 32 * 2^256 mod r in 8 x 32-bit words (Montgomery form of 32): x * C32 turns x * 2^256 into x * 2^261
 constexpr uint32_t C32[8] = {0x8fffff57u, 0x2fd4e156u, 0xa494b01au, 0x75bba827u,
                              0x819caa80u, 0x5301fa84u, 0x563d4475u, 0x0dc83629u};
+// record of R^2 (2^517 mod r, 29-bit limbs): mul29(x, TO_MONT) = x * 2^256 mod r, the Montgomery form
+constexpr uint32_t TO_MONT[9] = {0x142db4dfu, 0x19d6990eu, 0x1472f48cu, 0x06dbe7e3u, 0x0b84d579u,
+                                 0x10f9faf7u, 0x121f4380u, 0x17a112deu, 0x001275c7u};
 }  // namespace r29
 
 struct W29 {

@@ -20,11 +20,13 @@
 namespace kgs {
 
 constexpr int LC_MAX = 32;
+constexpr int LC_W29 = 10;  // words of a coefficient's 29-bit product record (fr29.hpp)
 struct LinComb {  // out[i] = sum_k coef_k * src_k[i] (zero beyond len_k) + (i == 0 ? c0 : 0)
   int nterms;
   const uint32_t* src[LC_MAX];
   uint64_t len[LC_MAX];
   uint32_t coef[LC_MAX][8];
+  uint32_t coef29[LC_MAX][LC_W29];  // coef_k as 29-bit records (prover.cpp fr29_record)
   uint32_t c0[8];
 };
 
@@ -60,10 +62,11 @@ struct MsmWork {
 // flight) or two (fastest alone) for the calling thread's later launches; returns the previous setting
 bool ntt_set_coresident(bool on);
 constexpr int TW29_WORDS = 10;  // words per 29-bit twiddle record (fr29.hpp W29_WORDS)
-// the 29-bit twiddle table (fr29.hpp, k_tw29 records) of an 8 x 32 stage table: the LDS passes of
-// ntt_dif / ntt_dit look up the table they were given and multiply by its 29-bit twin when registered
-void ntt_register_tw29(const uint32_t* tw, const uint32_t* tw29);
-void ntt_unregister_tw29(const uint32_t* tw);
+// the 29-bit twin (fr29.hpp, k_tw29 records; record i <-> element i) of `count` 8 x 32 elements at
+// `base`: the LDS passes of ntt_dif / ntt_dit multiply by the twin records of the twiddle table and
+// the pre / post scalings they were given when every one of them lies in a registered table
+void ntt_register_tw29(const uint32_t* base, uint64_t count, const uint32_t* twin);
+void ntt_unregister_tw29(const uint32_t* base);
 // out[i] = the k_tw29 record of in[i] (8 x 32 Montgomery words), i < count
 void launch_tw29(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t count);
 void ntt_dif(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t in_len, int logm, const uint32_t* pre,

@@ -265,12 +265,14 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
     if (i < N) {
       int32_t d[W];
       scalar_digits<C, true>(d, sc, i);  // sc: the standard forms k_sort_hist stored
+      // entry values are 32-bit (point index | sign bit 31): the index arithmetic in 32 bits
+      const uint32_t pidx = (uint32_t)pbase + (uint32_t)pstride * (uint32_t)i;
 #pragma unroll
       for (int j = 0; j < W; j++) {
         if (!d[j]) continue;
         const uint32_t k = (uint32_t)(d[j] < 0 ? -d[j] : d[j]);
         const uint32_t pos = atomicAdd(&cur[part_of(k, lob)], 1u);
-        sval[pos] = (uint32_t)((uint64_t)j * Nsrs + pbase + pstride * i) | (d[j] < 0 ? 0x80000000u : 0u);
+        sval[pos] = ((uint32_t)j * (uint32_t)Nsrs + pidx) | (d[j] < 0 ? 0x80000000u : 0u);
         skey[pos] = (uint16_t)(k - 1);
       }
     }
@@ -421,15 +423,24 @@ constexpr uint32_t SL_BIGRUN = 512;
 __device__ __forceinline__ void lo_write_runs(uint32_t* __restrict__ sorted, const uint32_t* sv, const uint32_t* n,
                                               const uint32_t* src, const uint32_t* dst, int nb, uint32_t* big,
                                               uint32_t* nbig) {
-  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // The bucket loop and each run's bounds are wave-uniform: read into scalar registers
+  // (readfirstlane), so the loop control and the run's base addresses are scalar work and a run of
+  // ~60 entries costs a few VALU (a lane-index compare and two offsets) instead of ~25 of per-bucket
+  // set-up in vector registers.
+  const uint32_t tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   for (uint32_t b = wave; b < (uint32_t)nb; b += SL_THREADS / 64) {
-    const uint32_t cnt = n[b];
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(n[b]);
     if (cnt > SL_BIGRUN) {
       if (lane == 0) big[atomicAdd(nbig, 1u)] = b;
       continue;
     }
-    const uint32_t s0 = src[b], d0 = dst[b];
-    for (uint32_t i = lane; i < cnt; i += 64) sorted[d0 + i] = sv[s0 + i];
+    const uint32_t s0 = __builtin_amdgcn_readfirstlane(src[b]), d0 = __builtin_amdgcn_readfirstlane(dst[b]);
+    const uint32_t* __restrict__ from = sv + s0;
+    uint32_t* __restrict__ to = sorted + d0;
+#pragma unroll 1
+    for (uint32_t i = 0; i < cnt; i += 64) {
+      if (i + lane < cnt) to[i + lane] = from[i + lane];
+    }
   }
   __syncthreads();
   const uint32_t nbg = *nbig;
@@ -489,10 +500,21 @@ __device__ __forceinline__ void lo_scatter_body(uint32_t* __restrict__ sorted, u
     // the chunk is one tile (every partition of a non-skewed MSM): each entry goes straight to its
     // slot (slot cursor per lo), then each bucket's run leaves with consecutive lanes
     __syncthreads();
+    // every entry's lo and value loaded first (all loads in flight at once), then the slot atomics
+    constexpr int PER = SL_TILE / SL_THREADS;
+    uint32_t lo_k[PER], val_k[PER];
 #pragma unroll
-    for (int k = 0; k < SL_TILE / SL_THREADS; k++) {
+    for (int k = 0; k < PER; k++) {
       const uint32_t e = c0 + tid + k * SL_THREADS;
-      if (e < c1) sv[atomicAdd(&toff[tlo[e]], 1u)] = tval[e];
+      if (e < c1) {
+        lo_k[k] = tlo[e];
+        val_k[k] = tval[e];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const uint32_t e = c0 + tid + k * SL_THREADS;
+      if (e < c1) sv[atomicAdd(&toff[lo_k[k]], 1u)] = val_k[k];
     }
     __syncthreads();
     lo_write_runs(sorted, sv, ccnt, coff, cur, nb, big, &nbig);

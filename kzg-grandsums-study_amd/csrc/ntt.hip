@@ -258,20 +258,26 @@ struct ntt_io {
   const uint32_t* post;  // last pass: times post[idx] and / or the scalar *post_s
   const uint32_t* post_s;
   int logm;
+  // the T29 passes: pre / post / post_s as 29-bit records (the domain's twin table, fr29.hpp)
+  const uint32_t* pre29;
+  const uint32_t* post29;
+  const uint32_t* post_s29;
 };
 
-template <bool DIT>
+// values in [0, 2p) (the butterflies' range): the scalings need no reduction below p
+template <bool DIT, bool T29>
 __device__ __forceinline__ fr ntt_load(const ntt_io& io, uint64_t idx) {
   if (!io.in) return fr::load(io.data + 8 * idx);
   if (DIT) return fr::load(io.in + 8 * (io.in_bitrev ? idx : (uint64_t)bitrev((uint32_t)idx, io.logm)));
   if (idx >= io.in_len) return fr::zero();
   fr x = fr::load(io.in + 8 * idx);
-  if (io.pre) x = x * fr::load(io.pre + 8 * idx);
+  if (io.pre) x = T29 ? mul29(x, w29_load(io.pre29 + TW29_WORDS * idx)) : x * fr::load(io.pre + 8 * idx);
   return x;
 }
+template <bool T29>
 __device__ __forceinline__ void ntt_store(const ntt_io& io, uint64_t idx, fr y) {
-  if (io.post) y = y * fr::load(io.post + 8 * idx);
-  if (io.post_s) y = y * fr::load(io.post_s);
+  if (io.post) y = T29 ? mul29(y, w29_load(io.post29 + TW29_WORDS * idx)) : y * fr::load(io.post + 8 * idx);
+  if (io.post_s) y = T29 ? mul29(y, w29_load(io.post_s29)) : y * fr::load(io.post_s);
   canon_out(y).store(io.data + 8 * idx);
 }
 
@@ -336,27 +342,35 @@ __device__ __forceinline__ void bfly_pair_x2(fr* x, int r0, int r1, int dist, co
 template <int R, bool DIT, bool GIN, bool GOUT, bool PF, typename TW>
 __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restrict__ tw, const ntt_io& io, uint32_t cl,
                                           uint32_t col, uint32_t jb, uint32_t js, int K, int logd, int lb, int kp0) {
+  constexpr bool T29 = std::is_same<TW, W29>::value;
   fr x[1 << R];
   if (GIN && !DIT && io.in && io.pre && R >= 2) {
     // first DIF pass with a coset pre-scaling: the products two at a time. A pair past the input
     // (the zero upper half of a degree < n polynomial on a 2n coset: the top j-bit, i.e. r >= 2^(R-1)
-    // for every lane) stays zero without its products
-#pragma unroll
-    for (int r = 0; r < (1 << R); r += 2) {
+    // for every lane) stays zero without its products. Compile-time register indices (static_for,
+    // see the step loop below): with the 29-bit products the unrolled loop went to scratch
+    static_for<(1 << R) / 2>([&](auto rc) {
+      constexpr int r = 2 * decltype(rc)::value;
       const uint32_t i0 = lds_idx(col, jb + js * r, K, logd), i1 = lds_idx(col, jb + js * (r + 1), K, logd);
       if (__builtin_expect(__all(i0 >= io.in_len && i1 >= io.in_len), 0)) {
         x[r] = fr::zero();
         x[r + 1] = fr::zero();
-        continue;
+        return;
       }
       const fr a0 = i0 < io.in_len ? fr::load(io.in + 8 * i0) : fr::zero();
       const fr a1 = i1 < io.in_len ? fr::load(io.in + 8 * i1) : fr::zero();
-      fr::mul_nored_x2(a0, fr::load(io.pre + 8 * i0), a1, fr::load(io.pre + 8 * i1), x[r], x[r + 1]);
-    }
+      if constexpr (T29) {
+        x[r] = mul29(a0, w29_load(io.pre29 + TW29_WORDS * i0));
+        x[r + 1] = mul29(a1, w29_load(io.pre29 + TW29_WORDS * i1));
+      } else {
+        fr::mul_nored_x2(a0, fr::load(io.pre + 8 * i0), a1, fr::load(io.pre + 8 * i1), x[r], x[r + 1]);
+      }
+    });
   } else {
-#pragma unroll
-    for (int r = 0; r < (1 << R); r++)
-      x[r] = GIN ? ntt_load<DIT>(io, lds_idx(col, jb + js * r, K, logd)) : lds_ld(lds, (jb + js * r) * lb + cl);
+    static_for<(1 << R)>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      x[r] = GIN ? ntt_load<DIT, T29>(io, lds_idx(col, jb + js * r, K, logd)) : lds_ld(lds, (jb + js * r) * lb + cl);
+    });
   }
 #ifndef KGS_NTT_SINGLE
   if constexpr (R >= 2) {
@@ -442,16 +456,29 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
   if (GOUT && R >= 2) {
     // last pass: the post-scalings two products at a time, then canonical stores
     if (io.post) {
-#pragma unroll
-      for (int r = 0; r < (1 << R); r += 2) {
+      static_for<(1 << R) / 2>([&](auto rc) {
+        constexpr int r = 2 * decltype(rc)::value;
         const uint32_t i0 = lds_idx(col, jb + js * r, K, logd), i1 = lds_idx(col, jb + js * (r + 1), K, logd);
-        fr::mul_nored_x2_ip(x[r], fr::load(io.post + 8 * i0), x[r + 1], fr::load(io.post + 8 * i1));
-      }
+        if constexpr (T29) {
+          x[r] = mul29(x[r], w29_load(io.post29 + TW29_WORDS * i0));
+          x[r + 1] = mul29(x[r + 1], w29_load(io.post29 + TW29_WORDS * i1));
+        } else {
+          fr::mul_nored_x2_ip(x[r], fr::load(io.post + 8 * i0), x[r + 1], fr::load(io.post + 8 * i1));
+        }
+      });
     }
     if (io.post_s) {
-      const fr ps = fr::load(io.post_s);
+      if constexpr (T29) {
+        const W29 ps = w29_load(io.post_s29);
+        static_for<(1 << R)>([&](auto rc) {
+          constexpr int r = decltype(rc)::value;
+          x[r] = mul29(x[r], ps);
+        });
+      } else {
+        const fr ps = fr::load(io.post_s);
 #pragma unroll
-      for (int r = 0; r < (1 << R); r += 2) fr::mul_nored_x2_ip(x[r], ps, x[r + 1], ps);
+        for (int r = 0; r < (1 << R); r += 2) fr::mul_nored_x2_ip(x[r], ps, x[r + 1], ps);
+      }
     }
 #pragma unroll
     for (int r = 0; r < (1 << R); r++) canon_out(x[r]).store(io.data + 8 * lds_idx(col, jb + js * r, K, logd));
@@ -460,7 +487,7 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
 #pragma unroll
   for (int r = 0; r < (1 << R); r++) {
     if (GOUT)
-      ntt_store(io, lds_idx(col, jb + js * r, K, logd), x[r]);
+      ntt_store<T29>(io, lds_idx(col, jb + js * r, K, logd), x[r]);
     else
       lds_st(lds, (jb + js * r) * lb + cl, x[r]);
   }
@@ -521,7 +548,7 @@ k_ntt_lds_pass(ntt_io io, const uint32_t* __restrict__ tw, int s0) {
     for (uint32_t e = threadIdx.x; e < LDS_ELEMS; e += LDS_NT) {
       uint32_t j, cl;
       lds_map(e, K, logd, LBLOG, j, cl);
-      lds_st(lds, j * LB + cl, ntt_load<DIT>(io, lds_idx(col0 + cl, j, K, logd)));
+      lds_st(lds, j * LB + cl, ntt_load<DIT, T29>(io, lds_idx(col0 + cl, j, K, logd)));
     }
     __syncthreads();
   }
@@ -541,7 +568,7 @@ k_ntt_lds_pass(ntt_io io, const uint32_t* __restrict__ tw, int s0) {
     for (uint32_t e = threadIdx.x; e < LDS_ELEMS; e += LDS_NT) {
       uint32_t j, cl;
       lds_map(e, K, logd, LBLOG, j, cl);
-      ntt_store(io, lds_idx(col0 + cl, j, K, logd), lds_ld(lds, j * LB + cl));
+      ntt_store<T29>(io, lds_idx(col0 + cl, j, K, logd), lds_ld(lds, j * LB + cl));
     }
   }
 }
@@ -549,27 +576,40 @@ k_ntt_lds_pass(ntt_io io, const uint32_t* __restrict__ tw, int s0) {
 // the calling thread's pass build (ntt_set_coresident; per thread: contexts prove on their callers' threads)
 thread_local bool g_ntt_coresident = false;
 
-// 8 x 32 stage table -> its registered 29-bit twin (the shared domain tables register theirs when
-// built, unregister when freed); KGS_NTT_T29=0 keeps the 8 x 32 products (A/B)
+// 8 x 32 element tables -> their registered 29-bit twins, record i of the twin = element i of the
+// table (the shared domain tables register theirs when built, unregister when freed): a pointer
+// anywhere inside a registered table (a stage table, the coset powers, one 1/m scalar) maps to its
+// record. KGS_NTT_T29=0 keeps the 8 x 32 products (A/B).
+struct Tw29Entry {
+  uint64_t count;
+  const uint32_t* twin;
+};
 static std::mutex g_tw29_mu;
-static std::map<const uint32_t*, const uint32_t*> g_tw29;
-void ntt_register_tw29(const uint32_t* tw, const uint32_t* tw29) {
+static std::map<const uint32_t*, Tw29Entry> g_tw29;
+void ntt_register_tw29(const uint32_t* base, uint64_t count, const uint32_t* twin) {
   std::lock_guard<std::mutex> lk(g_tw29_mu);
-  g_tw29[tw] = tw29;
+  g_tw29[base] = Tw29Entry{count, twin};
 }
-void ntt_unregister_tw29(const uint32_t* tw) {
+void ntt_unregister_tw29(const uint32_t* base) {
   std::lock_guard<std::mutex> lk(g_tw29_mu);
-  g_tw29.erase(tw);
+  g_tw29.erase(base);
 }
-static const uint32_t* tw29_of(const uint32_t* tw) {
+static bool t29_off() {
   static const bool off = [] {
     const char* e = getenv("KGS_NTT_T29");
     return e && e[0] == '0';
   }();
-  if (off) return nullptr;
+  return off;
+}
+static const uint32_t* tw29_of(const uint32_t* p) {
+  if (!p || t29_off()) return nullptr;
   std::lock_guard<std::mutex> lk(g_tw29_mu);
-  auto it = g_tw29.find(tw);
-  return it == g_tw29.end() ? nullptr : it->second;
+  auto it = g_tw29.upper_bound(p);
+  if (it == g_tw29.begin()) return nullptr;
+  --it;
+  const uint64_t off = (uint64_t)(p - it->first);
+  if (off % 8 || off / 8 >= it->second.count) return nullptr;
+  return it->second.twin + (uint64_t)TW29_WORDS * (off / 8);
 }
 
 // the 29-bit record of a stage twiddle (fr29.hpp): w * 2^261 mod p (= its Montgomery form times the
@@ -620,11 +660,16 @@ static void launch_lds_pass(hipStream_t st, int K, bool dit, uint32_t* data, con
                             int in_bitrev, const uint32_t* pre, const uint32_t* tw, int logm, int s0,
                             const uint32_t* post, const uint32_t* post_s) {
   const unsigned blocks = (unsigned)((1ull << logm) / LDS_ELEMS);
-  const ntt_io io{data, in, in_len, in_bitrev, pre, post, post_s, logm};
+  // the 29-bit twins of the twiddles and scalings, if the domain registered them: all or none
+  const uint32_t* pre29 = tw29_of(pre);
+  const uint32_t* post29 = tw29_of(post);
+  const uint32_t* post_s29 = tw29_of(post_s);
+  const uint32_t* tw29 = tw29_of(tw);
+  if ((pre && !pre29) || (post && !post29) || (post_s && !post_s29)) tw29 = nullptr;
+  const ntt_io io{data, in, in_len, in_bitrev, pre, post, post_s, logm, pre29, post29, post_s29};
   const int logd = dit ? s0 : logm - s0 - K;
   static const bool staged = getenv("KGS_NTT_STAGED") != nullptr;  // A/B: every pass staged through LDS
   const bool direct = logd >= NTT_ELOG - K && !staged;
-  const uint32_t* tw29 = tw29_of(tw);  // the 29-bit twin table, if the domain registered one
 #define KGS_LDS_LAUNCH2(A, B, C, D, E, T, TWP)                                                                 \
   do {                                                                                                         \
     if (g_ntt_coresident)                                                                                      \

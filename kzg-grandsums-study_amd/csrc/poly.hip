@@ -11,6 +11,7 @@
 // more 254-bit Montgomery products per element), the rest HBM bound.
 #include "kernels.hpp"
 #include "poly_math.hpp"
+#include "fr29.hpp"
 
 namespace kgs {
 
@@ -33,7 +34,11 @@ __global__ void k_to_mont(uint32_t* __restrict__ out, const uint32_t* __restrict
   KGS_AUX_PRIO();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  fr::load(in + 8 * i).to_mont().store(out + 8 * i);
+  // x * R as a 29-bit product by the constant record of R^2 (any x < 2^256; canonical output)
+  W29 r2;
+#pragma unroll
+  for (int j = 0; j < 9; j++) r2.l[j] = r29::TO_MONT[j];
+  fr::reduce_once(mul29(fr::load(in + 8 * i), r2)).store(out + 8 * i);
 }
 void launch_to_mont(hipStream_t st, uint32_t* out, const uint32_t* in, uint64_t n) {
   hipLaunchKernelGGL(k_to_mont, dim3(nb(n)), dim3(256), 0, st, out, in, n);
@@ -68,23 +73,24 @@ __global__ void k_lincomb(uint32_t* __restrict__ out, uint64_t n, LinComb lc) {
   KGS_AUX_PRIO();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  // the terms accumulate on [0, 2p) (29-bit products by the uniform coefficients, lazy sums), one
+  // canonicalisation at the end: the same canonical value as the term-by-term modular sum
   fr acc = fr::zero();
   for (int k = 0; k < lc.nterms; k++) {
     if (i < lc.len[k]) {
-      fr x = fr::load(lc.src[k] + 8 * i);
-      fr c;
+      W29 c;
 #pragma unroll
-      for (int j = 0; j < 8; j++) c.v[j] = lc.coef[k][j];
-      acc = acc + x * c;
+      for (int j = 0; j < 9; j++) c.l[j] = lc.coef29[k][j];
+      acc = fr::add_lazy(acc, mul29(fr::load(lc.src[k] + 8 * i), c));
     }
   }
   if (i == 0) {
     fr c;
 #pragma unroll
     for (int j = 0; j < 8; j++) c.v[j] = lc.c0[j];
-    acc = acc + c;
+    acc = fr::add_lazy(acc, c);
   }
-  acc.store(out + 8 * i);
+  fr::reduce_once(acc).store(out + 8 * i);
 }
 void launch_lincomb(hipStream_t st, uint32_t* out, uint64_t n, const LinComb& lc) {
   hipLaunchKernelGGL(k_lincomb, dim3(nb(n)), dim3(256), 0, st, out, n, lc);
@@ -383,7 +389,8 @@ void launch_builder(hipStream_t st, bool prod, bool sel, uint32_t* out, const ui
 // ---------------------------------------------------------------------------- quotient on a coset
 // Inputs: coset evaluations in bit-reversed order (size cs = 2^lcs) of S (or Z), F, T [, selF, selT].
 // rot = cs/n: S(w x_i) = S_eval[natural (i+rot) mod cs]. inv_nxm1[p] = 1/(n (x_i - 1)) (bitrev).
-// zinv[0|1] = 1/Z_H(x_i) for even/odd natural i (cs = 2n) or zinv[0] for all (cs = n).
+// zinv[0|1] = 1/Z_H(x_i) for even/odd natural i (cs = 2n) or zinv[0] for all (cs = n); k_quotient reads
+// alpha * zinv[0|1] as 29-bit records (slots 5-6, 7-8).
 template <bool PROD, bool SEL>
 __global__ void __launch_bounds__(256) k_quotient(uint32_t* __restrict__ q, const uint32_t* __restrict__ S,
                                                   const uint32_t* __restrict__ F, const uint32_t* __restrict__ T,
@@ -395,17 +402,17 @@ __global__ void __launch_bounds__(256) k_quotient(uint32_t* __restrict__ q, cons
   const uint64_t cs = 1ull << lcs;
   if (p >= cs) return;
   // scalars: alpha, gamma, zinv0, zinv1, alpha_t (selected only)
-  const fr alpha = fr::load(sc), gamma = fr::load(sc + 8), z0 = fr::load(sc + 16), z1 = fr::load(sc + 24);
+  const fr alpha = fr::load(sc), gamma = fr::load(sc + 8);
   const uint32_t i = brev((uint32_t)p, lcs);
   const uint32_t j = (i + rot) & (uint32_t)(cs - 1);
   const uint32_t pj = brev(j, lcs);
   const fr s = fr::load(S + 8 * p), sw = fr::load(S + 8 * (uint64_t)pj);
   const fr sf = SEL ? fr::load(SF + 8 * p) : fr::zero(), st = SEL ? fr::load(ST + 8 * p) : fr::zero();
-  fr acc = quotient_core<PROD, SEL>(s, sw, fr::load(F + 8 * p), fr::load(T + 8 * p), sf, st, alpha, gamma,
-                                            SEL ? fr::load(sc + 32) : fr::zero());
-  const fr zinv = (rot == 2 && (i & 1)) ? z1 : z0;
-  acc = acc * zinv + quotient_l1<PROD>(s, fr::load(inv_nxm1 + 8 * p));
-  acc.store(q + 8 * p);
+  const fr acc = quotient_core_na<PROD, SEL>(s, sw, fr::load(F + 8 * p), fr::load(T + 8 * p), sf, st, alpha, gamma,
+                                             SEL ? fr::load(sc + 32) : fr::zero());
+  // times alpha / Z_H(x_i) in one 29-bit product (records at scalar slots 5-6 / 7-8, prover.cpp)
+  const W29 az = w29_load(sc + ((rot == 2 && (i & 1)) ? 56 : 40));
+  (fr::reduce_once(mul29(acc, az)) + quotient_l1<PROD>(s, fr::load(inv_nxm1 + 8 * p))).store(q + 8 * p);
 }
 
 void launch_quotient(hipStream_t st, bool prod, bool sel, uint32_t* q, const uint32_t* S, const uint32_t* F,
@@ -436,10 +443,12 @@ __global__ void k_divcheck(uint32_t* __restrict__ flag, const uint32_t* __restri
   const fr alpha = fr::load(sc), gamma = fr::load(sc + 8);
   const fr s = fr::load(S + 8 * i), sw = i + 1 == n ? fr::load(S_next) : fr::load(S + 8 * (i + 1));
   const fr sf = SEL ? fr::load(sfp + 8 * i) : fr::zero(), st = SEL ? fr::load(stp + 8 * i) : fr::zero();
-  fr acc = quotient_core<PROD, SEL>(s, sw, fr::load(f + 8 * i), fr::load(t + 8 * i), sf, st, alpha, gamma,
-                                            SEL ? fr::load(sc + 32) : fr::zero());
-  if (gbase + i == 0) acc = acc + (PROD ? s - fr::one() : s);  // L1(w^0) = 1
-  if (!acc.is_zero()) atomicOr(flag, 1u);
+  const fr acc = quotient_core_na<PROD, SEL>(s, sw, fr::load(f + 8 * i), fr::load(t + 8 * i), sf, st, alpha, gamma,
+                                             SEL ? fr::load(sc + 32) : fr::zero());
+  // N(w^i) = alpha * acc (+ L1 S at w^0): away from w^0 it is zero iff alpha or acc is (no product)
+  const bool nz = gbase + i == 0 ? !(acc * alpha + (PROD ? s - fr::one() : s)).is_zero()  // L1(w^0) = 1
+                                 : !alpha.is_zero() && !acc.is_zero();
+  if (nz) atomicOr(flag, 1u);
 }
 
 void launch_divcheck(hipStream_t st, bool prod, bool sel, uint32_t* flag, const uint32_t* S, const uint32_t* f,
@@ -457,7 +466,8 @@ void launch_divcheck(hipStream_t st, bool prod, bool sel, uint32_t* flag, const 
 
 // ---------------------------------------------------------------------------- Horner tiles
 // part[poly][tile] = sum_{j in tile} c_j x^(j - tile_start); tile = 2048 coefficients.
-// xp[l] = x^(8 * 2^l), l = 0..7 ; x itself at xp[8]
+// xp[l] = x^(8 * 2^l), l = 0..7 ; x itself at xp[8], its 29-bit record at xp[10..11], xp[l]'s at
+// xp[12 + 2l] (prover.cpp xpowers)
 __global__ void __launch_bounds__(256) k_eval_tiles(uint32_t* __restrict__ part, EvalBatch eb,
                                                     const uint32_t* __restrict__ xp, uint32_t ntiles_max) {
   KGS_AUX_PRIO();
@@ -466,28 +476,33 @@ __global__ void __launch_bounds__(256) k_eval_tiles(uint32_t* __restrict__ part,
   const uint32_t* c = eb.src[pi];
   const uint64_t len = eb.len[pi];
   const uint64_t base = (uint64_t)blockIdx.x * BT_TILE + threadIdx.x * BT_PER;
-  const fr x = fr::load(xp + 8 * 8);
+  // Horner steps with x as a 29-bit record (xp[10..11]): h stays in [0, 2p), canonical after the loop
+  const W29 xw = w29_load(xp + 8 * 10);
   fr h = fr::zero();
 #pragma unroll
   for (int r = BT_PER - 1; r >= 0; r--) {
     uint64_t i = base + r;
     fr ci = i < len ? fr::load(c + 8 * i) : fr::zero();
-    h = h * x + ci;
+    h = mul29(h, xw) + ci;
   }
+  h = fr::reduce_once(h);
   // tree over the 256 partials, level l combining the previous level's pairs (2k, 2k+1) as
   // v_2k + v_2k+1 * x^(8*2^l) in threads k < 128 >> l: the active threads are contiguous, so whole
   // waves drop out (9 wave-products for the tree instead of 27 when thread t of every stride ran)
   h.store(lds + 8 * threadIdx.x);
   __syncthreads();
+  // (the level multipliers as 29-bit records, xp[12 + 2l]; partials on [0, 2p), canonical at the end)
   for (int l = 0, cnt = 128; l < 8; l++, cnt >>= 1) {
     const bool on = (int)threadIdx.x < cnt;
     fr v;
-    if (on) v = fr::load(lds + 8 * (2 * threadIdx.x)) + fr::load(lds + 8 * (2 * threadIdx.x + 1)) * fr::load(xp + 8 * l);
+    if (on)
+      v = fr::add_lazy(fr::load(lds + 8 * (2 * threadIdx.x)),
+                       mul29(fr::load(lds + 8 * (2 * threadIdx.x + 1)), w29_load(xp + 8 * (12 + 2 * l))));
     __syncthreads();
     if (on) v.store(lds + 8 * threadIdx.x);
     __syncthreads();
   }
-  if (threadIdx.x == 0) fr::load(lds).store(part + 8 * ((uint64_t)pi * ntiles_max + blockIdx.x));
+  if (threadIdx.x == 0) fr::reduce_once(fr::load(lds)).store(part + 8 * ((uint64_t)pi * ntiles_max + blockIdx.x));
 }
 
 void launch_eval_tiles(hipStream_t st, uint32_t* part, const EvalBatch& eb, const uint32_t* xp, uint32_t ntiles_max) {
@@ -533,13 +548,14 @@ __global__ void __launch_bounds__(SCAN_NT) k_div_carries(uint32_t* __restrict__ 
   }
 }
 
-// xp layout (shared with k_eval_tiles): xp[l] = z^(8*2^l) (l = 0..7), xp[8] = z, xp[9] = z^2048.
+// xp layout (shared with k_eval_tiles): xp[l] = z^(8*2^l) (l = 0..7), xp[8] = z, xp[9] = z^2048,
+// xp[10..11] = z's 29-bit record, xp[12 + 2l] = xp[l]'s record.
 __global__ void __launch_bounds__(256) k_div_finish(uint32_t* __restrict__ q, uint32_t* __restrict__ flag,
                                                     const uint32_t* __restrict__ a, uint64_t L,
                                                     const uint32_t* __restrict__ carry, const uint32_t* __restrict__ xp) {
   KGS_AUX_PRIO();
   __shared__ uint32_t lds[256 * 8];
-  const fr z = fr::load(xp + 8 * 8);
+  const W29 zw = w29_load(xp + 8 * 10);  // z as a 29-bit record
   const uint64_t base = (uint64_t)blockIdx.x * BT_TILE + threadIdx.x * BT_PER;
   fr av[BT_PER];
   fr h = fr::zero();
@@ -547,16 +563,19 @@ __global__ void __launch_bounds__(256) k_div_finish(uint32_t* __restrict__ q, ui
   for (int r = BT_PER - 1; r >= 0; r--) {
     uint64_t i = base + r;
     av[r] = i < L ? fr::load(a + 8 * i) : fr::zero();
-    h = h * z + av[r];
+    h = mul29(h, zw) + av[r];  // [0, 2p)
   }
+  h = fr::reduce_once(h);
   const fr cin_tile = fr::load(carry + 8 * (uint64_t)blockIdx.x);
   if (threadIdx.x == 255) h = h + fr::load(xp) * cin_tile;  // z^8 * carry
-  // inclusive suffix scan: V_t = h_t + z^8 V_{t+1}; at step l the multiplier is z^(8*2^l)
+  // inclusive suffix scan: V_t = h_t + z^8 V_{t+1}; at step l the multiplier is z^(8*2^l) (its
+  // 29-bit record xp[12 + 2l]; partials on [0, 2p), reduced where they are used below)
   for (int l = 0; l < 8; l++) {
     const int off = 1 << l;
     h.store(lds + 8 * threadIdx.x);
     __syncthreads();
-    if (threadIdx.x + off < 256) h = h + fr::load(xp + 8 * l) * fr::load(lds + 8 * (threadIdx.x + off));
+    if (threadIdx.x + off < 256)
+      h = fr::add_lazy(h, mul29(fr::load(lds + 8 * (threadIdx.x + off)), w29_load(xp + 8 * (12 + 2 * l))));
     __syncthreads();
   }
   h.store(lds + 8 * threadIdx.x);
@@ -565,7 +584,7 @@ __global__ void __launch_bounds__(256) k_div_finish(uint32_t* __restrict__ q, ui
 #pragma unroll
   for (int k = BT_PER - 1; k >= 0; k--) {
     uint64_t i = base + k;
-    r = av[k] + z * r;  // r_i
+    r = av[k] + fr::reduce_once(mul29(r, zw));  // r_i, canonical
     if (i < L) {
       if (i >= 1) r.store(q + 8 * (i - 1));
       else if (!r.is_zero()) atomicOr(flag, 1u);

@@ -11,11 +11,11 @@
 
 namespace kgs {
 
-// alpha * (sel terms + main term); L1 part added by the caller
+// sel terms + main term, before the outer factor alpha (k_quotient folds alpha into 1/Z_H)
 template <bool PROD, bool SEL>
-__device__ __forceinline__ fr quotient_core(const fr& s, const fr& sw, const fr& fv, const fr& tv, const fr& sf,
-                                            const fr& st, const fr& alpha, const fr& gamma,
-                                            const fr& alpha_t) {
+__device__ __forceinline__ fr quotient_core_na(const fr& s, const fr& sw, const fr& fv, const fr& tv, const fr& sf,
+                                               const fr& st, const fr& alpha, const fr& gamma,
+                                               const fr& alpha_t) {
   const fr fg = fv + gamma, tg = tv + gamma;
   fr acc = fr::zero();
   if (SEL) {
@@ -37,7 +37,14 @@ __device__ __forceinline__ fr quotient_core(const fr& s, const fr& sw, const fr&
     }
     q1 = sw * dT - s * dF;
   }
-  return (acc + q1) * alpha;
+  return acc + q1;
+}
+// alpha * (sel terms + main term); L1 part added by the caller
+template <bool PROD, bool SEL>
+__device__ __forceinline__ fr quotient_core(const fr& s, const fr& sw, const fr& fv, const fr& tv, const fr& sf,
+                                            const fr& st, const fr& alpha, const fr& gamma,
+                                            const fr& alpha_t) {
+  return quotient_core_na<PROD, SEL>(s, sw, fv, tv, sf, st, alpha, gamma, alpha_t) * alpha;
 }
 
 // L1(x) S(x) / Z_H(x) with L1/Z_H = 1/(n(x - 1)) = nxm1; grand-product uses Z(x) - 1

@@ -120,23 +120,21 @@ void ensure_domain(kgs_ctx& c, int logM) {
   }
   launch_powers(c.st, d->coset_pow, M, dc + 16 * logM, nullptr);
   launch_powers(c.st, d->coset_ipow, M, dc + 16 * logM + 8, nullptr);
-  // 29-bit twins of the stage tables for the LDS passes' products (fr29.hpp)
-  HC(dev_malloc((void**)&d->mem29, (size_t)4 * 2 * TW29_WORDS * M));
-  d->tw29_fwd = d->mem29;
-  d->tw29_inv = d->mem29 + (size_t)TW29_WORDS * M;
-  launch_tw29(c.st, d->tw29_fwd, d->tw_fwd, M);
-  launch_tw29(c.st, d->tw29_inv, d->tw_inv, M);
   std::vector<Fr> im(logM + 1);
   for (int l = 0; l <= logM; l++) im[l] = Fr::from_u64(1ull << l).inverse();
   uint8_t* h = c.pin(32 * (logM + 1));
   for (int l = 0; l <= logM; l++) im[l].to_bytes(h + 32 * l);
   HC(hipMemcpyAsync(d->invm, h, 32 * (logM + 1), hipMemcpyHostToDevice, c.st));
+  // the 29-bit twin of every table (stage twiddles, coset powers, 1/m), record i <-> element i, for
+  // the LDS passes' products (fr29.hpp)
+  const uint64_t entries = 4 * M + logM + 1;
+  HC(dev_malloc((void**)&d->mem29, (size_t)4 * TW29_WORDS * entries));
+  launch_tw29(c.st, d->mem29, d->mem, entries);
   check_launch();
   c.sync();  // built: publish
   c.h_pin_off = pin_mark;
   c.d_scal_off = scal_mark;
-  ntt_register_tw29(d->tw_fwd, d->tw29_fwd);
-  ntt_register_tw29(d->tw_inv, d->tw29_inv);
+  ntt_register_tw29(d->mem, entries, d->mem29);
   d->logM = logM;
   g_dom_reg.erase(std::remove_if(g_dom_reg.begin(), g_dom_reg.end(), [](auto& w) { return w.expired(); }),
                   g_dom_reg.end());
@@ -471,14 +469,34 @@ void commit_finish(kgs_ctx& c, const Commit& cm, uint8_t out[64]) { commits_fini
 // ------------------------------------------------------------------ Horner evaluation
 // returns p_j(x) for each poly of the batch
 
+// The 29-bit product record of a constant (fr29.hpp mul29): x * 2^261 mod r (x's Montgomery form times
+// 32) in 9 x 29-bit limbs + zero pad, as two 32-byte scalar slots; the per-element kernels multiply by
+// a uniform constant with it (one mad per partial product, no carry words)
+void fr29_record(const Fr& x, Fr out[2]) {
+  const Fr y = x * Fr::from_u64(32);
+  uint32_t w[16] = {0};
+  for (int j = 0; j < 9; j++) {
+    const int bit = 29 * j, i = bit >> 6, off = bit & 63;
+    uint64_t l = y.v[i] >> off;
+    if (off > 35 && i + 1 < 4) l |= y.v[i + 1] << (64 - off);
+    w[j] = (uint32_t)(l & 0x1fffffffu);
+  }
+  memcpy(out[0].v, w, 32);
+  memcpy(out[1].v, w + 8, 32);
+}
+
+// xp[l] = x^(8 * 2^l) (l < 8), xp[8] = x, xp[9] = x^2048, xp[10..11] = the 29-bit record of x,
+// xp[12 + 2l .. 13 + 2l] = the record of xp[l] (l < 8)
 uint32_t* xpowers(kgs_ctx& c, const Fr& x) {
-  Fr p[10];
+  Fr p[28];
   Fr x8 = x.sqr().sqr().sqr();
   p[0] = x8;
   for (int l = 1; l < 8; l++) p[l] = p[l - 1].sqr();
   p[8] = x;
   p[9] = p[7].sqr();  // x^2048
-  return c.scal(p, 10);
+  fr29_record(x, p + 10);
+  for (int l = 0; l < 8; l++) fr29_record(p[l], p + 12 + 2 * l);
+  return c.scal(p, 28);
 }
 
 EvalJob eval_launch(kgs_ctx& c, const std::vector<const uint32_t*>& src, const std::vector<uint64_t>& len, const Fr& x,
@@ -534,12 +552,18 @@ void run_lincomb(hipStream_t st, uint32_t* out, uint64_t n, const LcTerms& t) {
       lc.src[0] = out;
       lc.len[0] = n;
       Fr::one().to_bytes((uint8_t*)lc.coef[0]);
+      Fr rec[2];
+      fr29_record(Fr::one(), rec);
+      memcpy(lc.coef29[0], rec, 4 * LC_W29);
       lc.nterms = 1;
     }
     for (; k < t.src.size() && lc.nterms < LC_MAX; k++) {
       lc.src[lc.nterms] = t.src[k];
       lc.len[lc.nterms] = t.len[k];
       t.coef[k].to_bytes((uint8_t*)lc.coef[lc.nterms]);
+      Fr rec[2];
+      fr29_record(t.coef[k], rec);
+      memcpy(lc.coef29[lc.nterms], rec, 4 * LC_W29);
       lc.nterms++;
     }
     (first ? t.c0 : Fr::zero()).to_bytes((uint8_t*)lc.c0);
@@ -891,9 +915,12 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   // alpha_t: weight of the selT-binary term (none for a lookup, whose selT holds multiplicities)
   // 1/Z_H on the two coset halves, times 1/cs (the scaling of the inverse transform below; nxm1 carries it too)
   const Fr inv_cs = Fr::from_u64(cs).inverse();
-  Fr qs[5] = {alpha, gamma, (gn - Fr::one()).inverse() * inv_cs, (gn.neg() - Fr::one()).inverse() * inv_cs,
+  Fr qs[9] = {alpha, gamma, (gn - Fr::one()).inverse() * inv_cs, (gn.neg() - Fr::one()).inverse() * inv_cs,
               lk ? Fr::zero() : alpha};
-  uint32_t* d_qs = c.scal(qs, 5);
+  // k_quotient: alpha / Z_H on each coset half as one 29-bit product record (slots 5-6, 7-8)
+  fr29_record(alpha * qs[2], qs + 5);
+  fr29_record(alpha * qs[3], qs + 7);
+  uint32_t* d_qs = c.scal(qs, 9);
   launch_divcheck(c.st, !gs, sel, flags + 1, Sev, fcomb, tcomb, in.sel_f, in.sel_t, d_qs, n);
   const uint32_t* Qc = c.buf("Qc", 32 * cs);
   launch_quotient(c.st, !gs, sel, (uint32_t*)Qc, cosS, cosF, cosT, cosSF, cosST, nxm1, d_qs, lcs, rot);

@@ -11,7 +11,9 @@ import glob
 import os
 import sys
 
-ONE_TIME = ("k_tab_dbl", "k_batch_affine", "k_tab_to29", "k_fixed_base", "k_powers", "k_nxm1")
+# one-time per context / domain (SRS tables, domain tables, the cached 1/(n(x-1)) of get_nxm1)
+ONE_TIME = ("k_tab_dbl", "k_batch_affine", "k_tab_to29", "k_fixed_base", "k_powers", "k_nxm1", "k_fr_batch_inv",
+            "k_tw29")
 
 
 def main():

@@ -43,6 +43,8 @@ def test_constants():
     assert R % (1 << 28) == 1 and INV == INV32 == (1 << 28) - 1
     c32 = _arr("C32", T)
     assert sum(w << (32 * i) for i, w in enumerate(c32)) == (32 << 256) % R
+    tm = _arr("TO_MONT", T)  # k_to_mont's record: mul29(x, TO_MONT) = x * 2^256
+    assert all(x <= MASK for x in tm) and sum(x << (29 * j) for j, x in enumerate(tm)) == pow(2, 517, R)
 
 
 def unpack(x):
