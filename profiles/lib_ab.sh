@@ -1,10 +1,10 @@
-# Same-box A/B of the in-tree library against kzg-grandsums-study_amd/lib_ab/libkgs_prev.so (the previous
+# Same-box A/B of the in-tree library against kzg-grandsums-study_amd/lib_ab/prev/libkgs.so (the previous
 # commit's build): proofs in flight, device-resident, interleaved reps
 # usage: bash profiles/lib_ab.sh [reps=3]
 set -e
 for rep in $(seq 1 ${1:-3}); do
   for v in new prev; do
-    if [ $v = new ]; then unset KGS_LIB; else export KGS_LIB=$PWD/kzg-grandsums-study_amd/lib_ab/libkgs_prev.so; fi
+    if [ $v = new ]; then unset KGS_LIB; else export KGS_LIB=$PWD/kzg-grandsums-study_amd/lib_ab/prev/libkgs.so; fi
     echo "== rep $rep library $v"
     timeout -k 10 120 python -u profiles/host_inflight.py 20 4 48 1 device
   done
