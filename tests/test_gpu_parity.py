@@ -98,6 +98,51 @@ def test_ntt_large_vs_c_oracle(ctx9, logm):
         assert ctx9.ntt(x, inverse) == C.ntt(x, inverse), inverse
 
 
+_T32 = """
+import hashlib, json, sys
+sys.path.insert(0, {tests!r})
+import numpy as np
+import common
+K = common.load_pkg()
+c = K.Context(0)
+out = {{}}
+for logm in (11, 14, 17, 20, 21):
+    rng = np.random.Generator(np.random.PCG64(100 + logm))
+    w = rng.integers(0, 2**64 - 1, size=(1 << logm, 4), dtype=np.uint64, endpoint=True)
+    w[:, 3] &= np.uint64((1 << 60) - 1)
+    x = w.tobytes()
+    out[str(logm)] = [hashlib.sha256(c.ntt(x, inv)).hexdigest() for inv in (False, True)]
+path = "/tmp/kgs_test_t32_p13.ptau"
+c.write_synthetic_ptau(path, 13, common.tau())
+c.load_ptau(path, 12)
+rng = np.random.Generator(np.random.PCG64(7))
+f = rng.integers(0, 2**64 - 1, size=(1 << 12, 4), dtype=np.uint64, endpoint=True)
+f[:, 3] &= np.uint64((1 << 60) - 1)
+t = np.roll(f, 1, axis=0)
+coms, evs, mf, mt = c.prove(K.GRANDSUM, 12, [f.tobytes()], [t.tobytes()])
+out["proof"] = hashlib.sha256(b"".join(coms) + b"".join(evs)).hexdigest()
+print(json.dumps(out))
+"""
+
+
+def test_ntt_8x32_products_identical():
+    """The NTT LDS passes multiply by 29-bit twiddle / scaling records (fr29.hpp) by default and by the
+    8 x 32-bit words with KGS_NTT_T29=0: both builds give the same transforms (2^11..2^21, forward and
+    inverse with 1/m) and the same proof (coset transforms of the quotient), each in a fresh process
+    (the knob is read once per process)."""
+    import json
+    import subprocess
+    import sys
+    code = _T32.format(tests=os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for t29 in ("1", "0"):
+        env = dict(os.environ, KGS_NTT_T29=t29)
+        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+        assert out.returncode == 0, out.stderr[-3000:]
+        res.append(json.loads(out.stdout.strip().splitlines()[-1]))
+    assert res[0] == res[1]
+
+
 def test_msm(ctx9):
     srs = P.SRS(common.oracle_ptau(9), common.tau())
     rnd = random.Random(2)
