@@ -12,7 +12,9 @@
 // Arithmetic: butterflies run on values in [0, 2p) (lazy reduction, fr::add_lazy / sub_lazy /
 // sub_2p / mul_nored): one conditional correction per sum or difference and none after a product;
 // every pass stores canonical values, so the output is bit-identical to a canonical-arithmetic
-// network. -DKGS_NTT_CANON builds the canonical butterflies (A/B).
+// network. -DKGS_NTT_CANON builds the canonical butterflies (A/B). Since round 5 the LDS passes
+// multiply by 29-bit records of their twiddles and scalings (fr29.hpp mul29: the domain's twin
+// tables, same [0, 2p) contract); KGS_NTT_T29=0 selects the 8 x 32-bit products.
 //
 // Twiddles: per direction one resident STAGE table tw[h + t] = w_{2h}^t (t < h, h = 1..M/2; M
 // entries for the largest domain M), so the butterflies of one stage read consecutive twiddles
