@@ -55,6 +55,11 @@ def test_to_mont(ctx9):
     rnd = random.Random(1)
     v = rv(rnd, 777)
     assert ctx9.fr_to_mont(common.std_bytes(v)) == common.mont_bytes(v)
+    # non-canonical standard forms (r <= x < 2^256): the Evaluations buffers are read mod r (oracle
+    # protocol.Evaluations.std_values); k_to_mont's 29-bit product takes any x < 2^256
+    raw = [R, R + 1, 2 * R - 1, 5 * R - 1, (1 << 256) - 1] + [rnd.randrange(R, 1 << 256) for _ in range(300)]
+    b = b"".join(x.to_bytes(32, "little") for x in raw)
+    assert ctx9.fr_to_mont(b) == common.mont_bytes([x % R for x in raw])
 
 
 def test_from_mont_and_batch_inverse(ctx9):
