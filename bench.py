@@ -25,7 +25,9 @@ Extra fields in the JSON line:
               (prover.js:147-148) — PCIe-inclusive, so never `value`; `vs_device_resident` is its ratio
               to `value`, and the host path's proof must equal the device path's
   host_buffer_boundary : single-proof latency of kgs_prove on pageable host buffers (median / spread of
-              7) and of the JavaScript drop-in module (javascript_module: median / spread of its samples)
+              7) and of the JavaScript drop-in module (javascript_module: the library default, V8
+              collecting on its own schedule; javascript_module_app_eager_gc: the application's opt-in,
+              node --expose-gc + KGS_JS_EAGER_GC=1, one collection beside the GPU work of a lone proof)
   latency_ms_single_proof / latency_single_proof_ms / round_ms_single_proof : one proof at a time on one
               context (2 MSM lanes), device-resident inputs, median and spread of 7
   msm       : live HIP-event timing of the MSM phases at N = n (points/s, G1 adds/s)
@@ -504,8 +506,20 @@ def main():
                                       str(nbits), "7",
                                       str(4 * args.inflight)], capture_output=True, text=True, timeout=300, env=env)
                 host_leg["javascript_module"] = json.loads(out.stdout.strip().splitlines()[-1])
+                # the same single-proof samples with the application's opt-in eager collection
+                # (the module never changes V8 flags or collects by default)
+                env["KGS_JS_EAGER_GC"] = "1"
+                out = subprocess.run(["node", "--expose-gc", os.path.join(js_dir, "test", "time_prove.js"), ptau,
+                                      str(nbits), "7", "0"], capture_output=True, text=True, timeout=300, env=env)
+                eg = json.loads(out.stdout.strip().splitlines()[-1])
+                host_leg["javascript_module_app_eager_gc"] = {
+                    "ms_per_proof": eg["ms_per_proof"], "latency_ms": eg["latency_ms"], "verified": eg["verified"],
+                    "best_inside_libkgs": eg["best_inside_libkgs"],
+                    "note": "node --expose-gc with KGS_JS_EAGER_GC=1 (the application's opt-in): one full V8 "
+                            "collection 5 ms after a lone proof is queued, beside its GPU work; 7 single proofs"}
             except Exception as e:  # the JS leg must not hide the GPU number
-                host_leg["javascript_module"] = {"error": str(e)[:200]}
+                host_leg.setdefault("javascript_module", {"error": str(e)[:200]})
+                host_leg.setdefault("javascript_module_app_eager_gc", {"error": str(e)[:200]})
 
     msm = roofline = hbm_view = cpu = None
     extra_cfg = {}
