@@ -260,10 +260,13 @@ def test_srs_loaded_by_need(K):
 
 @pytest.mark.parametrize("kind", ["grandsum", "grandproduct"])
 @pytest.mark.parametrize("sel", [False, True])
-def test_twelve_multisets(K, kind, sel):
-    """k = 12 vectors (above the 10 of round 1; the reference bounds nPols nowhere): byte-exact vs
-    the oracle — linear combinations and evaluation batches run in several launches."""
-    nbits, k = 3, 12
+@pytest.mark.parametrize("k", [12, 20])
+def test_twelve_multisets(K, kind, sel, k):
+    """k = 12 and 20 vectors (above the 10 of round 1; the reference bounds nPols nowhere): byte-exact
+    vs the oracle — linear combinations (k = 20: more terms than one launch's LC_MAX = 32, so the
+    chained launches re-read the partial sum through its 29-bit record of 1) and evaluation batches
+    run in several launches."""
+    nbits = 3
     ptau = common.oracle_ptau(9)
     srs = P.SRS(ptau, common.tau())
     Fs, Ts, sF, sT = common.make_inputs(1200 + sel, nbits, k, sel)
