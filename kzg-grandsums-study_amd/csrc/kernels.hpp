@@ -3,12 +3,14 @@
 // unless stated otherwise. Launches are asynchronous on `st`.
 #pragma once
 
-// Wave priority: every kernel except k_accumulate raises its waves to priority 1, so the short latency-bound
-// kernels of the other in-flight proofs (NTT, sort, MSM tail, poly) win VALU arbitration against the long
-// accumulate waves they share SIMDs with (arbitration is by priority, then age). A/B on MI355X, same box:
-// 77.9 -> 80.5 proofs/s at n = 2^20 (4 in flight); single-proof latency 14.6 -> 14.9 ms. -DKGS_NO_PRIO_AUX disables.
+// Wave priority: every kernel except k_accumulate raises its waves to priority 3 (1 until round 5), so the
+// short latency-bound kernels of the other in-flight proofs (NTT, sort, MSM tail, poly) win VALU arbitration
+// against the long accumulate waves they share SIMDs with (arbitration is by priority, then age); the
+// accumulate waves stay at 0, or step 2 -> 1 -> 0 with their progress (msm.hip, k_accumulate). A/B on
+// MI355X, same box: 77.9 -> 80.5 proofs/s at n = 2^20 (4 in flight); single-proof latency 14.6 -> 14.9 ms.
+// -DKGS_NO_PRIO_AUX disables.
 #ifndef KGS_NO_PRIO_AUX
-#define KGS_AUX_PRIO() __builtin_amdgcn_s_setprio(1)
+#define KGS_AUX_PRIO() __builtin_amdgcn_s_setprio(3)
 #else
 #define KGS_AUX_PRIO() ((void)0)
 #endif

@@ -637,6 +637,7 @@ __device__ __forceinline__ const uint32_t* run_rec(const uint32_t* raw, uint64_t
 // ran (kgs_diag_clock), also with other proofs' kernels in flight. Stamps go to their own buffer.
 constexpr int KGS_CLK_BLOCKS = 8192;
 __device__ unsigned long long g_kgs_clk[4 * KGS_CLK_BLOCKS];
+__device__ unsigned int g_kgs_clk_cu[KGS_CLK_BLOCKS];
 #endif
 template <int VW>
 __global__ void __launch_bounds__(256, VW) k_accumulate(uint32_t* __restrict__ segowner,
@@ -644,7 +645,7 @@ __global__ void __launch_bounds__(256, VW) k_accumulate(uint32_t* __restrict__ s
                                                     const uint32_t* __restrict__ sorted,
                                                     const uint32_t* __restrict__ offsets, uint32_t nbins,
                                                     const uint32_t* __restrict__ table, uint32_t L,
-                                                    uint32_t* __restrict__ raw) {
+                                                    uint32_t* __restrict__ raw, uint32_t prio_m1, uint32_t prio_m2) {
   if (VW == 2) asm volatile("; reserve v175 (176 VGPRs: two waves per SIMD)" ::: "v175");
   const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t E = offsets[nbins];
@@ -689,7 +690,18 @@ __global__ void __launch_bounds__(256, VW) k_accumulate(uint32_t* __restrict__ s
   uint32_t vn = sorted[start + 1 <= last ? start + 1 : last];
   const uint4* pt = reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(v & KGS_DIAG_GATHER_MASK));
   uint4 a0 = pt[0], a1 = pt[1], a2 = pt[2], a3 = pt[3];
-  for (uint32_t e = (uint32_t)start; e <= last; e++) {
+  // Progress priority (prio_m1 != 0): a SIMD's VALU goes to the oldest of its ready waves at equal
+  // priority, so of two accumulate waves with the same L entries the older finishes first and the
+  // younger then runs alone, without a partner to hide its latencies (alone on the GPU: the earlier
+  // block of a CU finishes at ~57 % of the launch, profiles/acc_residency.py). Each wave lowers its
+  // priority 2 -> 1 -> 0 after prio_m1 and prio_m2 entries, so a wave that is a level behind is issued
+  // first; the late second step leaves little work for the last, equal-priority stretch, after which
+  // the younger wave runs alone. The aux kernels run at 3, above every accumulate wave.
+  uint32_t it = 0;
+  if (prio_m1) __builtin_amdgcn_s_setprio(2);
+  for (uint32_t e = (uint32_t)start; e <= last; e++, it++) {
+    if (it == prio_m1) __builtin_amdgcn_s_setprio(1);
+    if (it == prio_m2) __builtin_amdgcn_s_setprio(0);
     const uint4* pn = reinterpret_cast<const uint4*>(table + 16 * (uint64_t)(vn & KGS_DIAG_GATHER_MASK));
     const uint4 n0 = pn[0], n1 = pn[1], n2 = pn[2], n3 = pn[3];
     const uint32_t vnn = sorted[e + 2 <= last ? e + 2 : last];
@@ -721,6 +733,9 @@ __global__ void __launch_bounds__(256, VW) k_accumulate(uint32_t* __restrict__ s
     o[1] = clk1;
     o[2] = rt0;
     o[3] = rt1;
+    unsigned int xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_kgs_clk_cu[blockIdx.x] = ((xcc & 15u) << 16) | (unsigned int)__smid();
   }
 #endif
 }
@@ -743,6 +758,23 @@ extern "C" int kgs_diag_lorec(unsigned long long* out, unsigned int cap, unsigne
 }
 
 // median over the stamped blocks of d(shader clock) / d(real time) x 100 MHz, in GHz
+// raw stamps of the last accumulate launch: per block {clk0, clk1, rt0, rt1, cu}; returns the count
+extern "C" int kgs_diag_clock_raw(unsigned long long* out, int max) {
+  static unsigned long long h[4 * KGS_CLK_BLOCKS];
+  static unsigned int cu[KGS_CLK_BLOCKS];
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_kgs_clk), sizeof(h)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(cu, HIP_SYMBOL(g_kgs_clk_cu), sizeof(cu)) != hipSuccess) return -1;
+  int n = 0;
+  for (int b = 0; b < KGS_CLK_BLOCKS && n < max; b++) {
+    if (!(h[4 * b + 3] > h[4 * b + 2])) continue;
+    for (int k = 0; k < 4; k++) out[5 * n + k] = h[4 * b + k];
+    out[5 * n + 4] = cu[b];
+    n++;
+  }
+  return n;
+}
+
 extern "C" int kgs_diag_clock(double* ghz, int* nblocks) {
   static unsigned long long h[4 * KGS_CLK_BLOCKS];
   if (hipDeviceSynchronize() != hipSuccess) return 1;
@@ -991,12 +1023,21 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   uint32_t* cnt = w.chunkcnt;
   const uint64_t lcap = nseg / CB_T + B + 16;
   hipMemsetAsync(cnt, 0, 4 * CB_LEVELS, st);
+  // progress priority (k_accumulate): KGS_ACC_PRIO 0 off, 1 the exclusive (two-lane) build, 2 every launch
+  static const int acc_prio = [] {
+    const char* e = getenv("KGS_ACC_PRIO");
+    return e ? atoi(e) : 1;
+  }();
+  // steps at 3/4 and 93/100 of the segment (a two-wave issue model with the leftover rate of the
+  // younger wave measured alone, 0.34 of the older's, puts these within 1 % of the best pair)
+  const bool prio = acc_prio >= 2 || (acc_prio == 1 && exclusive_acc);
+  const uint32_t pm1 = prio ? (uint32_t)(3 * L / 4) : 0u, pm2 = prio ? (uint32_t)(93 * L / 100) : 0u;
   if (exclusive_acc)
     hipLaunchKernelGGL(k_accumulate<2>, dim3(nb(nseg)), dim3(256), 0, st, w.segowner, w.chunklist, cnt, w.sorted,
-                       w.offsets, B + 1, tb.table, (uint32_t)L, w.raw29);
+                       w.offsets, B + 1, tb.table, (uint32_t)L, w.raw29, pm1, pm2);
   else
     hipLaunchKernelGGL(k_accumulate<3>, dim3(nb(nseg)), dim3(256), 0, st, w.segowner, w.chunklist, cnt, w.sorted,
-                       w.offsets, B + 1, tb.table, (uint32_t)L, w.raw29);
+                       w.offsets, B + 1, tb.table, (uint32_t)L, w.raw29, pm1, pm2);
   if (ev) hipEventRecord(ev[2], st);  // the accumulate phase is the k_accumulate launch alone
   uint64_t stride = 1, cap = lcap;
   for (int j = 0; j < CB_LEVELS; j++, stride *= CB_T) {

@@ -17,7 +17,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "kzg-grandsums-study_amd", "csrc")
-SYM = "_ZN3kgs12k_accumulateILi3EEEvPjS1_S1_PKjS3_jS3_jS1_"
+SYM = "_ZN3kgs12k_accumulateILi3EEEvPjS1_S1_PKjS3_jS3_jS1_j"
 
 
 def compile_asm(src_dir, out):
