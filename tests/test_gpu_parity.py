@@ -148,6 +148,53 @@ def test_ntt_8x32_products_identical():
     assert res[0] == res[1]
 
 
+_PRIO = """
+import hashlib, json, sys
+sys.path.insert(0, {tests!r})
+import numpy as np
+import common
+K = common.load_pkg()
+out = {{}}
+path = "/tmp/kgs_test_prio_p17.ptau"
+c = K.Context(0)
+c.write_synthetic_ptau(path, 17, common.tau())
+c.load_ptau(path, 17)
+rng = np.random.Generator(np.random.PCG64(11))
+for nb in (12, 16, 17):
+    w = rng.integers(0, 2**64 - 1, size=(1 << nb, 4), dtype=np.uint64, endpoint=True)
+    w[:, 3] &= np.uint64((1 << 60) - 1)
+    for lanes in (2, 1):
+        c.set_msm_lanes(lanes)
+        out[f"msm{{nb}}/{{lanes}}"] = c.msm(w.tobytes()).hex()
+c.set_msm_lanes(2)
+f = rng.integers(0, 2**64 - 1, size=(1 << 14, 4), dtype=np.uint64, endpoint=True)
+f[:, 3] &= np.uint64((1 << 60) - 1)
+t = np.roll(f, 1, axis=0)
+coms, evs, mf, mt = c.prove(K.GRANDSUM, 14, [f.tobytes()], [t.tobytes()])
+out["proof"] = hashlib.sha256(b"".join(coms) + b"".join(evs)).hexdigest()
+print(json.dumps(out))
+"""
+
+
+def test_accumulate_priority_identical():
+    """The accumulate's progress-stepped wave priority (KGS_ACC_PRIO: 1 = two-lane contexts, the
+    default; 0 = off; 2 = every launch) only reorders issue: MSMs of 2^12..2^17 points on two-lane and
+    one-lane contexts and a 2^14 proof are identical under all three, each in a fresh process (the
+    knob is read once per process)."""
+    import json
+    import subprocess
+    import sys
+    code = _PRIO.format(tests=os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for prio in ("1", "0", "2"):
+        env = dict(os.environ, KGS_ACC_PRIO=prio)
+        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+        assert out.returncode == 0, out.stderr[-3000:]
+        res.append(json.loads(out.stdout.strip().splitlines()[-1]))
+    assert res[0] == res[1] == res[2]
+    assert res[0]["msm16/2"] == res[0]["msm16/1"]
+
+
 def test_msm(ctx9):
     srs = P.SRS(common.oracle_ptau(9), common.tau())
     rnd = random.Random(2)
