@@ -564,14 +564,20 @@ def main():
         achieved = mults / (acc_ms / 1e3) / 1e9
         peak = MAD_PEAK / MADS_PER_PRODUCT_29 / 1e9
         peak32 = MAD_PEAK / MADS_PER_PRODUCT_32 / 1e9
-        traffic = None
+        # HBM bytes per launch from the committed counter passes: FETCH_SIZE doubled (the guide's gfx950
+        # correction: FETCH_SIZE tallies 128 B requests at 64 B) + WRITE_SIZE is `traffic`; the raw
+        # FETCH_SIZE + WRITE_SIZE sum is reported beside it
+        traffic = traffic_raw = None
         pmc_path = os.path.join(HERE, "profiles", "pmc_accumulate.json")
         if os.path.exists(pmc_path):
             try:
                 with open(pmc_path) as fh:
-                    traffic = json.load(fh).get("hbm_bytes_per_launch")
+                    pj = json.load(fh)
+                traffic_raw = pj.get("hbm_bytes_per_launch")
+                if pj.get("fetch_bytes_x2_corrected") is not None and pj.get("write_bytes") is not None:
+                    traffic = pj["fetch_bytes_x2_corrected"] + pj["write_bytes"]
             except Exception:
-                traffic = None
+                traffic = traffic_raw = None
         # the clock the chip holds under this kernel and its achieved SIMD cycles per VALU instruction,
         # from a committed counter pass (profiles/clock_accumulate.json; GRBM_GUI_ACTIVE / 8 / duration)
         clock = None
@@ -585,6 +591,12 @@ def main():
         roofline = {"bound": "valu", "kernel": "k_accumulate", "achieved": round(achieved, 2), "peak": round(peak, 2),
                     "unit": "G Fq-products/s", "frac": round(achieved / peak, 4),
                     "peak_8x32": round(peak32, 2), "frac_8x32": round(achieved / peak32, 4), "traffic": traffic,
+                    "traffic_raw_fetch_plus_write": traffic_raw,
+                    "traffic_vs_algorithmic": round(traffic / (68 * entries.value), 3) if traffic else None,
+                    "traffic_note": "HBM bytes per 2^20-point launch from the FETCH_SIZE / WRITE_SIZE passes "
+                                    "(profiles/pmc_accumulate.json): FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE; "
+                                    "above the 68 B/entry algorithmic bytes because each 64 B table point is a "
+                                    "random gather",
                     "peak_note": f"v_mad_u64_u32 issue rate ({MAD_CYCLES} SIMD cycles per wave64 instruction, 256 CUs x 4 "
                                  f"SIMDs, 2.4 GHz) / mads per product: 162 (9 x 29-bit, peak) or 128 (8 x 32-bit, peak_8x32)",
                     "bound_note": "integer-VALU issue bound (254-bit Montgomery products on v_mad_u64_u32): neither the "
@@ -613,7 +625,7 @@ def main():
         b_proof = (4192 if args.kind == "grandsum" else 101 * 32) * n
         hbm_view = {"algorithmic_bytes_per_proof": b_proof, "achieved_GBps": round(b_proof * value / 1e9, 1),
                     "peak_GBps": 8000.0, "frac": round(b_proof * value / 1e9 / 8000.0, 4),
-                    "accumulate_pmc_GBps": round(traffic / (acc_ms / 1e3) / 1e9, 1) if traffic else None,
+                    "accumulate_pmc_GBps": round(traffic / (acc_ms / 1e3) / 1e9, 1) if traffic else None,  # corrected
                     "note": "the proof is INT-VALU bound (MSM bucket accumulation), not HBM bound"}
 
         # ---------------- CPU baseline (oracle/c port of the reference op list), N = 1 only
@@ -623,7 +635,10 @@ def main():
             try:
                 sys.path.insert(0, HERE)
                 from oracle import cbackend
-                cpu = cbackend.cpu_baseline(nbits, args.kind, threads=args.cpu_threads, ptau=ptau)
+                # the same multiset as context 0's timed proofs, and its last proof compared byte for
+                # byte with the GPU's (coms0 / evs0, device-resident path)
+                cpu = cbackend.cpu_baseline(nbits, args.kind, threads=args.cpu_threads, ptau=ptau,
+                                            inputs=(hbufs[0][0], hbufs[0][1]), expect=(coms0, evs0))
             except Exception as e:  # baseline failure must not hide the GPU number
                 cpu = {"error": str(e)[:200]}
 

@@ -224,6 +224,11 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
  * (profiles/r03/boundary_ab.txt): register only buffers that outlive several proofs. */
 int kgs_host_register(void* ptr, uint64_t bytes);
 int kgs_host_unregister(void* ptr);
+/* Every kgs_prove / kgs_prove_device call returns with none of its transfers or kernels pending, on
+ * its error paths too (a failed call drains the context's streams before it returns), so a caller may
+ * unregister or free its buffers as soon as the call returns. kgs_ctx_idle reports 1 when no stream
+ * of the context has work outstanding, 0 otherwise (diagnostic; the tests check the contract). */
+int kgs_ctx_idle(kgs_ctx_t* ctx);
 /* Same with device-resident inputs (HIP device pointers on ctx's device). */
 int kgs_prove_device(kgs_ctx_t* ctx, int kind, int nbits, int npols, const void* const* d_evals_f,
                      const void* const* d_evals_t, const void* d_sel_f, const void* d_sel_t, uint8_t* commitments_out,

@@ -87,6 +87,7 @@ def lib():
         L.kgs_host_register.argtypes = [c_u8p, ctypes.c_uint64]
         L.kgs_host_unregister.argtypes = [c_u8p]
         L.kgs_last_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+        L.kgs_ctx_idle.argtypes = [ctypes.c_void_p]
         L.kgs_fr_to_mont.argtypes = [ctypes.c_void_p, c_u8p, c_u8p, ctypes.c_uint64]
         L.kgs_fr_from_mont.argtypes = [ctypes.c_void_p, c_u8p, c_u8p, ctypes.c_uint64]
         L.kgs_fr_batch_inverse.argtypes = [ctypes.c_void_p, c_u8p, c_u8p, ctypes.c_uint64]
@@ -522,6 +523,12 @@ class Context:
         lib().kgs_last_exchange(self._h, arr, 6)
         return {"alltoall_n": int(arr[0]), "alltoall_ms": arr[1], "alltoall_bytes": int(arr[2]),
                 "allgather_n": int(arr[3]), "allgather_ms": arr[4], "allgather_bytes": int(arr[5])}
+
+    def idle(self):
+        """True when none of the context's streams has work outstanding (kgs_ctx_idle)."""
+        rc = lib().kgs_ctx_idle(self._h)
+        _check(rc)
+        return rc == 1
 
     def last_timing(self):
         arr = (ctypes.c_double * 9)()

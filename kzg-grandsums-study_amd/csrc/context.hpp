@@ -141,6 +141,10 @@ struct kgs_group {
   virtual void allgather(int rank, const void* send, void* recv, size_t bytes) = 0;
   // device all-to-all ordered on st: chunk j of send -> rank j; chunk j of recv <- rank j
   virtual void alltoall(int rank, struct kgs_ctx& c, hipStream_t st, const void* send, void* recv, size_t chunk) = 0;
+  // bytes that leave a rank in one alltoall of `chunk`-byte chunks on this transport: the chunks for
+  // the W - 1 other ranks, unless the transport moves more (HostGroup without an all-to-all callback
+  // all-gathers the whole send buffer)
+  virtual uint64_t alltoall_wire_bytes(size_t chunk) const { return (uint64_t)chunk * (world - 1); }
   // a rank failed: unblock the others (they fail too instead of waiting forever)
   virtual void abort() {}
   // a context on `device` becomes `rank` (kgs_ctx_set_group): transports that move device data
@@ -241,11 +245,19 @@ struct kgs_ctx {
 
   ~kgs_ctx() {
     hipSetDevice(device);
-    // every stream may still read pool buffers or pinned staging: drain all before freeing
-    if (st) hipStreamSynchronize(st);
-    if (st2) hipStreamSynchronize(st2);
-    if (st_copy) hipStreamSynchronize(st_copy);
-    if (st_wb) hipStreamSynchronize(st_wb);
+    // every stream may still read pool buffers or pinned staging: drain all before freeing. A drain
+    // that fails is reported here, naming the stream: HIP errors are sticky, and unreported the fault
+    // would surface at the next checked call of whatever runs next in the process (round 5's fault
+    // surfaced that way in the NEXT test's first copy, profiles/r05/boundary/feed_per_piece_dma_fault.log)
+    const char* names[4] = {"main", "lane 2", "input copy", "write-back"};
+    const hipStream_t ss[4] = {st, st2, st_copy, st_wb};
+    for (int i = 0; i < 4; i++) {
+      if (!ss[i]) continue;
+      const hipError_t e = hipStreamSynchronize(ss[i]);
+      if (e != hipSuccess)
+        fprintf(stderr, "kgs: context on device %d: its %s stream failed while draining at destruction: %s\n", device,
+                names[i], hipGetErrorString(e));
+    }
     for (auto& kv : pool) hipFree(kv.second.p);
     if (h_pin) hipHostFree(h_pin);
     if (h_io) hipHostFree(h_io);
@@ -377,7 +389,9 @@ struct kgs_ctx {
 namespace kgsi {
 
 // ------------------------------------------------------------------ building blocks (prover.cpp)
-void ensure_domain(kgs_ctx& c, int logM);
+// twin: also the tables' 29-bit twin (false only for the reference-quirks replay's growth)
+void ensure_domain(kgs_ctx& c, int logM, bool twin = true);
+void ensure_twin(kgs_ctx& c);  // the context's domain gets its twin if it was grown without one
 uint32_t* get_nxm1(kgs_ctx& c, int nbits, int lcs);
 void intt_nat(kgs_ctx& c, uint32_t* out, const uint32_t* in, int logm, hipStream_t st = nullptr);
 // coefficients (len <= 2^lcs) -> coset evaluations p(g w^i), bit-reversed order

@@ -1030,7 +1030,12 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   }();
   // steps at 3/4 and 93/100 of the segment (a two-wave issue model with the leftover rate of the
   // younger wave measured alone, 0.34 of the older's, puts these within 1 % of the best pair)
+#ifdef KGS_NO_PRIO_AUX
+  const bool prio = false;  // the A/B build without wave priorities: no step priority either
+  (void)acc_prio;
+#else
   const bool prio = acc_prio >= 2 || (acc_prio == 1 && exclusive_acc);
+#endif
   const uint32_t pm1 = prio ? (uint32_t)(3 * L / 4) : 0u, pm2 = prio ? (uint32_t)(93 * L / 100) : 0u;
   if (exclusive_acc)
     hipLaunchKernelGGL(k_accumulate<2>, dim3(nb(nseg)), dim3(256), 0, st, w.segowner, w.chunklist, cnt, w.sorted,

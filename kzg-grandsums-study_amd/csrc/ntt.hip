@@ -374,8 +374,14 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
       x[r] = GIN ? ntt_load<DIT, T29>(io, lds_idx(col, jb + js * r, K, logd)) : lds_ld(lds, (jb + js * r) * lb + cl);
     });
   }
-#ifndef KGS_NTT_SINGLE
-  if constexpr (R >= 2) {
+#ifdef KGS_NTT_SINGLE
+  // A/B build: one butterfly at a time. That path reads 8 x 32-bit twiddles only, so the 29-bit
+  // instantiations keep the pairs (select KGS_NTT_T29=0 to measure the single path everywhere)
+  constexpr bool kPairs = T29;
+#else
+  constexpr bool kPairs = true;
+#endif
+  if constexpr (R >= 2 && kPairs) {
     // Butterflies two at a time (q, q + half), their products interleaved (fr::mul_nored_x2; four at a
     // time, fr::mul_nored_x4 at 232 VGPRs, measured 1.25x slower: profiles/r03/ntt_x2_x4.txt). A pair
     // whose twiddles are all w^0 = 1 across the wave (low stages of the contiguous pass, where t depends
@@ -433,9 +439,7 @@ __device__ __forceinline__ void lds_round(uint32_t* lds, const uint32_t* __restr
         bfly_pair_x2<DIT>(x, r0, r1, dist, tw_load<TW>(tw, tw0[st]), tw_load<TW>(tw, tw1[st]));
       }
     });
-  } else
-#endif
-  {
+  } else {
     static_assert(sizeof(TW) == sizeof(fr), "the single-butterfly path reads 8 x 32-bit twiddles only");
 #pragma unroll
     for (int k = 0; k < R; k++) {

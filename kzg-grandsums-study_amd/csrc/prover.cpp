@@ -53,11 +53,15 @@ using host::Fr;
 namespace kgsi {
 
 // Every device allocation goes through here. KGS_DEBUG_ALLOC_LIMIT=<bytes> (fault injection for the
-// tests) makes any single request above that size fail as out-of-memory.
+// tests) makes any single request above that size fail as out-of-memory; with KGS_DEBUG_ALLOC_RANK=<r>
+// only on the host thread that is proving as rank r of a rank group (a failure on ONE rank of an
+// in-process group, whose ranks are threads of one process).
+thread_local int tl_group_rank = -1;
 hipError_t dev_malloc(void** p, size_t bytes) {
   if (const char* e = getenv("KGS_DEBUG_ALLOC_LIMIT")) {
     const unsigned long long lim = strtoull(e, nullptr, 10);
-    if (lim && bytes > lim) {
+    const char* rk = getenv("KGS_DEBUG_ALLOC_RANK");
+    if (lim && bytes > lim && (!rk || atoi(rk) == tl_group_rank)) {
       *p = nullptr;
       return hipErrorOutOfMemory;
     }
@@ -74,13 +78,34 @@ std::vector<std::weak_ptr<DomainTables>> g_dom_reg;
 namespace kgsi {
 
 // ------------------------------------------------------------------ domain tables
+// The 29-bit twin of every table (stage twiddles, coset powers, 1/m), record i <-> element i, for the
+// LDS passes' products (fr29.hpp): 40 B per element beside the 32 B words. Built with the domain for
+// the proofs' own domains; a domain grown only for the reference-quirks replay (up to 2^26 points)
+// gets none (its NTTs take the 8 x 32 products, the same values), and the first proof that runs on it
+// builds the twin then (ensure_twin). Under g_reg_mu.
+static void build_twin(kgs_ctx& c, DomainTables* d) {
+  if (d->mem29) return;
+  const uint64_t entries = 4 * (1ull << d->logM) + d->logM + 1;
+  HC(dev_malloc((void**)&d->mem29, (size_t)4 * TW29_WORDS * entries));
+  launch_tw29(c.st, d->mem29, d->mem, entries);
+  check_launch();
+  HC(hipStreamSynchronize(c.st));
+  ntt_register_tw29(d->mem, entries, d->mem29);
+}
+void ensure_twin(kgs_ctx& c) {
+  if (!c.dom || c.dom->mem29) return;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  build_twin(c, c.dom.get());
+}
+
 // Shared per device: a context asking for 2^logM reuses any published table of at least that size.
-void ensure_domain(kgs_ctx& c, int logM) {
+void ensure_domain(kgs_ctx& c, int logM, bool twin) {
   if (c.logM >= logM) return;
   std::lock_guard<std::mutex> lk(g_reg_mu);
   for (auto& w : g_dom_reg) {
     auto d = w.lock();
     if (d && d->device == c.device && d->logM >= logM) {
+      if (twin) build_twin(c, d.get());
       c.use_domain(d);
       c.nxm1.clear();
       return;
@@ -125,17 +150,12 @@ void ensure_domain(kgs_ctx& c, int logM) {
   uint8_t* h = c.pin(32 * (logM + 1));
   for (int l = 0; l <= logM; l++) im[l].to_bytes(h + 32 * l);
   HC(hipMemcpyAsync(d->invm, h, 32 * (logM + 1), hipMemcpyHostToDevice, c.st));
-  // the 29-bit twin of every table (stage twiddles, coset powers, 1/m), record i <-> element i, for
-  // the LDS passes' products (fr29.hpp)
-  const uint64_t entries = 4 * M + logM + 1;
-  HC(dev_malloc((void**)&d->mem29, (size_t)4 * TW29_WORDS * entries));
-  launch_tw29(c.st, d->mem29, d->mem, entries);
   check_launch();
-  c.sync();  // built: publish
+  c.sync();  // built
   c.h_pin_off = pin_mark;
   c.d_scal_off = scal_mark;
-  ntt_register_tw29(d->mem, entries, d->mem29);
   d->logM = logM;
+  if (twin) build_twin(c, d.get());  // then publish
   g_dom_reg.erase(std::remove_if(g_dom_reg.begin(), g_dom_reg.end(), [](auto& w) { return w.expired(); }),
                   g_dom_reg.end());
   g_dom_reg.push_back(d);
@@ -644,6 +664,7 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   if (in.kind == KGS_LOOKUP && !in.sel_f)
     throw KgsError(KGS_E_ARG, "a lookup needs both selectors (sel_t holds the multiplicities)");
   c.xs.reset();
+  ensure_twin(c);  // a domain last grown by a quirks replay has no 29-bit twin yet
   if (c.group) {
     prove_dist_group(c, in, com_out, ev_out);
     return;
@@ -657,8 +678,9 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
   } ntt_mode(c.msm_lanes < 2);
   using clk = std::chrono::steady_clock;
   auto t0 = clk::now();
-  c.timing.resize(9, 0.0);
-  for (int r = 0; r < 6; r++) c.timing[r] = 0.0;
+  // every slot, the host-boundary ones [6..8] too: kgs_prove writes them after this returns, and a
+  // device-resident proof must not report a previous host call's copy and prover times
+  c.timing.assign(9, 0.0);
   Range range(ROUND_NAMES[0]);
   auto lap = [&](int r) {
     auto t1 = clk::now();
@@ -1386,14 +1408,23 @@ static unsigned copy_threads() {
   return n;
 }
 namespace {
+// Invariants (DESIGN.md §5 "Round 6: the round-5 fault"): a piece is claimed exactly once, before
+// par_copy returns, and pool threads make no HIP call (every DMA is enqueued by the thread that owns
+// the call, after par_copy returned). Queue entries outlive their task (a helper that wakes late pops a
+// finished task): such a late `work()` must claim nothing, which `closed` checks.
 struct CopyTask {
   std::vector<CopyJob> pieces;
   std::atomic<size_t> next{0}, done{0};
+  std::atomic<bool> closed{false};  // set once par_copy has seen every piece done
   std::mutex mu;
   std::condition_variable cv;
   void work() {
     size_t i, mine = 0;
     while ((i = next.fetch_add(1)) < pieces.size()) {
+      if (closed.load(std::memory_order_acquire)) {
+        fprintf(stderr, "kgs: copy piece %zu claimed after its task completed\n", i);
+        abort();
+      }
       memcpy(pieces[i].dst, pieces[i].src, pieces[i].len);
       mine++;
     }
@@ -1453,6 +1484,7 @@ void par_copy(const std::vector<CopyJob>& jobs) {
   task->work();
   std::unique_lock<std::mutex> lk(task->mu);
   task->cv.wait(lk, [&] { return task->done.load() == task->pieces.size(); });
+  task->closed.store(true, std::memory_order_release);
 }
 
 // Caller buffers the DMAs can read / write in place: memory the caller already pinned (hipHostMalloc,
@@ -1466,6 +1498,22 @@ void par_copy(const std::vector<CopyJob>& jobs) {
 // proofs): the registrations are reference-counted process-wide, so the first call to finish does not
 // unpin memory another call is still DMA-ing. Overlapping buffers with different starts fail to
 // register and take the staging path.
+// Drains every stream of the context when the call it guards leaves by an exception. Rank-group
+// contexts are left alone: their main stream may wait in an exchange whose peers failed (the group's
+// abort releases it), and they never DMA caller memory in place.
+struct DrainOnError {
+  kgs_ctx* ctx;
+  int unwinding = std::uncaught_exceptions();
+  explicit DrainOnError(kgs_ctx* c) : ctx(c) {}
+  ~DrainOnError() {
+    if (std::uncaught_exceptions() <= unwinding || ctx->group) return;
+    hipSetDevice(ctx->device);
+    for (hipStream_t s : {ctx->st, ctx->st2, ctx->st_copy, ctx->st_wb})
+      if (s) (void)hipStreamSynchronize(s);
+    (void)hipGetLastError();
+  }
+};
+
 static std::mutex g_pin_mu;
 static std::map<void*, std::pair<size_t, int>> g_pins;  // start -> (bytes, calls holding it)
 struct HostPins {
@@ -1542,6 +1590,21 @@ int kgs_host_unregister(void* ptr) {
   API_END
 }
 
+int kgs_ctx_idle(kgs_ctx_t* ctx) {
+  API_BEGIN
+  if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");
+  CTX_LOCK(ctx);
+  HC(hipSetDevice(ctx->device));
+  for (hipStream_t s : {ctx->st, ctx->st2, ctx->st_copy, ctx->st_wb}) {
+    if (!s) continue;
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipErrorNotReady) return 0;
+    HC(e);
+  }
+  return 1;
+  API_END
+}
+
 int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* const* evals_f,
               const uint8_t* const* evals_t, const uint8_t* sel_f, const uint8_t* sel_t, uint8_t* const* mont_f,
               uint8_t* const* mont_t, uint8_t* commitments_out, uint8_t* evaluations_out) {
@@ -1551,6 +1614,10 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   if ((sel_f == nullptr) != (sel_t == nullptr)) throw KgsError(KGS_E_ARG, "selectors must be both given or both NULL");
   if (npols < 1 || npols > KGS_MAX_POLS || nbits < 1 || nbits > 28) throw KgsError(KGS_E_ARG, "bad shape");
   HC(hipSetDevice(ctx->device));
+  // declared first, so destroyed last (after the feeder and the write-back thread are joined): an
+  // error return drains the context's streams, so no DMA of this call still reads or writes caller
+  // memory (pinned inputs DMA'd in place, pinned write-back targets) once the caller has it back
+  DrainOnError drain(ctx);
   const uint64_t n = 1ull << nbits;
   const size_t E = 32 * n;
   ProveIn in;
@@ -1748,6 +1815,7 @@ int kgs_prove_device(kgs_ctx_t* ctx, int kind, int nbits, int npols, const void*
   if ((d_sel_f == nullptr) != (d_sel_t == nullptr)) throw KgsError(KGS_E_ARG, "selectors must be both given or both NULL");
   if (npols < 1 || npols > KGS_MAX_POLS || nbits < 1 || nbits > 28) throw KgsError(KGS_E_ARG, "bad shape");
   HC(hipSetDevice(ctx->device));
+  DrainOnError drain(ctx);  // no kernel of a failed call still reads the caller's device buffers
   ProveIn in;
   in.kind = kind;
   in.nbits = nbits;

@@ -143,6 +143,9 @@ struct HostGroup : kgs_group {
   void allgather(int, const void* send, void* recv, size_t bytes) override {
     if (fn(user, (const uint8_t*)send, (uint8_t*)recv, bytes) != 0) throw KgsError(KGS_E_COMM, "group all-gather failed");
   }
+  uint64_t alltoall_wire_bytes(size_t chunk) const override {
+    return a2a_fn ? (uint64_t)chunk * (world - 1) : (uint64_t)chunk * world * (world - 1);
+  }
   void alltoall(int rank, kgs_ctx&, hipStream_t st, const void* send, void* recv, size_t chunk) override {
     const size_t bytes = chunk * world;
     if (h_send.size() < bytes) h_send.resize(bytes);
@@ -272,7 +275,7 @@ struct Dist {
     HC(hipEventRecord(ev.first, c.st));
     g.alltoall(r, c, c.st, send, recv, (size_t)32 * chunk_elems);
     HC(hipEventRecord(ev.second, c.st));
-    x.a2a_bytes += (uint64_t)32 * chunk_elems * (W - 1);
+    x.a2a_bytes += g.alltoall_wire_bytes((size_t)32 * chunk_elems);  // what the transport moved
   }
   void allgather(const void* s, void* rv, size_t b) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -709,7 +712,10 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
     bool need = false;
     for (uint64_t d : deg) need |= d >= 1 && 2 * d < n;
     if (need) {
-      c.dist_err_agreed = true;  // a failure of the replay is the same on every rank
+      // Only the replay's own decisions are the same on every rank (made from the gathered full
+      // operands): its semantic errors (exempt in prove_dist_group anyway) and its "reference-quirks
+      // mode:" refusals. A HIP or allocation failure in the gathers, the domain growth or the replay is
+      // this rank's alone, stays un-agreed and aborts the group.
       const uint32_t* fF = D.gather_cyc(polF, M, "d_rq_F");
       const uint32_t* fT = D.gather_cyc(polT, M, "d_rq_T");
       const uint32_t* fS = D.gather_cyc(Sc, M, "d_rq_S");
@@ -717,18 +723,27 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
       const uint32_t* fST = sel ? D.gather_cyc(sTc, M, "d_rq_ST") : nullptr;
       uint32_t* fmut = nullptr;
       uint64_t qlen_ref = 0;
-      const uint32_t* Qref = ref_quirks_quotient(c, gs, sel, lk, nbits, alpha, gamma, fF, fT, fS, fSF, fST, qlen_ref, fmut);
-      if (fmut)
+      const uint32_t* Qref = nullptr;
+      try {
+        Qref = ref_quirks_quotient(c, gs, sel, lk, nbits, alpha, gamma, fF, fT, fS, fSF, fST, qlen_ref, fmut);
+      } catch (const KgsError& e) {
+        if (e.code == KGS_E_ARG && e.what() && !strncmp(e.what(), "reference-quirks mode:", 22)) c.dist_err_agreed = true;
+        throw;
+      }
+      if (fmut) {
+        c.dist_err_agreed = true;
         throw KgsError(KGS_E_ARG, "reference-quirks mode: the replay wrote into polF's buffer (Q2); not reproduced by a rank group");
-      if (qlen_ref > cs)
+      }
+      if (qlen_ref > cs) {
+        c.dist_err_agreed = true;
         throw KgsError(KGS_E_ARG, "reference-quirks mode: the reference's Q has more coefficients than the group's coset layout");
+      }
       // this rank's CYCLIC slice of the reference's Q (coefficients r + W j)
       HC(hipMemsetAsync(Qc, 0, 32 * Mc, c.st));
       const uint64_t cnt = qlen_ref > (uint64_t)r ? (qlen_ref - r + W - 1) / W : 0;
       if (cnt) HC(hipMemcpy2DAsync(Qc, 32, Qref + 8 * r, (size_t)32 * W, 32, cnt, hipMemcpyDeviceToDevice, c.st));
       qlen = qlen_ref;
       replayed = true;
-      c.dist_err_agreed = false;
     }
   }
   Commit cQ = commit_cyc(Qc, qlen);
@@ -916,9 +931,15 @@ void prove_dist_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* e
 // the group usable too; anything else happened on this rank alone mid-proof and aborts the group, so
 // that the other ranks fail at their next exchange instead of waiting in it (RCCL: at the
 // KGS_GROUP_TIMEOUT_S deadline of RcclGroup::wait).
+extern thread_local int tl_group_rank;  // prover.cpp dev_malloc: per-rank fault injection
 void prove_dist_group(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out) {
   c.xs.reset();
   c.dist_err_agreed = false;
+  struct RankTag {
+    int prev;
+    explicit RankTag(int r) : prev(tl_group_rank) { tl_group_rank = r; }
+    ~RankTag() { tl_group_rank = prev; }
+  } tag(c.group_rank);
   dist_preconditions(c, in);
   try {
     prove_dist_impl(c, in, com_out, ev_out);

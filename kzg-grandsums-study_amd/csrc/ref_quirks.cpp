@@ -145,7 +145,7 @@ struct Engine {
                                     std::to_string(REF_LOG_MAX));
     if (logm > c.logM) {
       HC(hipStreamSynchronize(st));
-      ensure_domain(c, logm);
+      ensure_domain(c, logm, false);  // replay-only growth: no 29-bit twin
     }
   }
   // Evaluations.fromPolynomial(a, factor) (evaluations.js:12-18): a zero-padded to 2^logB, forward

@@ -89,35 +89,46 @@ def msm(srs_bytes, scalars_mont, threads=0):
     return out.raw
 
 
-def cpu_baseline(nbits, kind="grandsum", threads=0, ptau=None, max_seconds=90.0, reps=3):
-    """Time the C port on the bench workload (same generator as bench.py) as BASELINE.md:84-87
-    prescribes: 1 warm-up proof, then the median of `reps` (>= 3) timed proofs, with their spread.
-    If the warm-up alone shows that warm-up + reps would exceed `max_seconds`, fewer timed proofs are
-    run (at least one) and the sample says so. Returns the bench.py `cpu_baseline` object."""
+def cpu_baseline(nbits, kind="grandsum", threads=0, ptau=None, max_seconds=90.0, reps=3, inputs=None, expect=None):
+    """Time the C port on the bench workload as BASELINE.md:84-87 prescribes: 1 warm-up proof, then
+    the median of `reps` (>= 3) timed proofs, with their spread. If the warm-up alone shows that
+    warm-up + reps would exceed `max_seconds`, fewer timed proofs are run (at least one) and the
+    sample says so. `inputs` = (F list, T list) of standard-form bytes: exactly the multiset of the GPU's timed proofs
+    (bench.py passes context 0's); default: the bench generator's first multiset. `expect` = the GPU
+    proof (commitments, evaluations) of those inputs: the last CPU proof is compared with it byte for
+    byte (`proof_identical`). Returns the bench.py `cpu_baseline` object."""
     import numpy as np
     n = 1 << nbits
-    rng = np.random.Generator(np.random.PCG64(0x4B5A4753))
-    w = rng.integers(0, np.iinfo(np.uint64).max, size=(n, 4), dtype=np.uint64, endpoint=True)
-    w[:, 3] &= np.uint64((1 << 61) - 1)
-    f = np.ascontiguousarray(w).view(np.uint8).reshape(n, 32)
-    t = np.roll(f, 1, axis=0)
+    if inputs is None:
+        rng = np.random.Generator(np.random.PCG64(0x4B5A4753))
+        w = rng.integers(0, np.iinfo(np.uint64).max, size=(n, 4), dtype=np.uint64, endpoint=True)
+        w[:, 3] &= np.uint64((1 << 61) - 1)
+        f = np.ascontiguousarray(w).view(np.uint8).reshape(n, 32)
+        t = np.roll(f, 1, axis=0)
+        inputs = ([f.tobytes()], [t.tobytes()])
     _, srs = load_srs_bytes(ptau)
     kk = 0 if kind == "grandsum" else 1
     if threads <= 0:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    fb, tb = [f.tobytes()], [t.tobytes()]
+    fb, tb = [bytes(x) for x in inputs[0]], [bytes(x) for x in inputs[1]]
+    last = {}
 
     def one():
         t0 = time.perf_counter()
-        prove_raw(kk, nbits, fb, tb, None, None, srs, threads)
+        last["proof"] = prove_raw(kk, nbits, fb, tb, None, None, srs, threads)
         return time.perf_counter() - t0
     warm = one()
     k = max(1, min(reps, int((max_seconds - warm) // max(warm, 1e-9))))
     times = sorted(one() for _ in range(k))
+    identical = None
+    if expect is not None:
+        identical = list(last["proof"][0]) == list(expect[0]) and list(last["proof"][1]) == list(expect[1])
     med = times[len(times) // 2] if len(times) % 2 else 0.5 * (times[len(times) // 2 - 1] + times[len(times) // 2])
     return {"value": round(1.0 / med, 5), "unit": "proofs/s", "cores": threads, "kind": "port",
             "median_s_per_proof": round(med, 3), "min_s": round(times[0], 3), "max_s": round(times[-1], 3),
             "spread_pct": round(100.0 * (times[-1] - times[0]) / med, 1), "warmup_s": round(warm, 3),
-            "sample": f"1 warm-up + median of {k} full {kind} proof(s) at n=2^{nbits}, k=1 (oracle/c C restatement "
-                      f"of the reference op list incl. 4n multiply, OpenMP {threads} threads): {med:.2f} s/proof "
+            "proof_identical": identical,
+            "sample": f"1 warm-up + median of {k} full {kind} proof(s) at n=2^{nbits}, k={len(fb)} (oracle/c C restatement "
+                      f"of the reference op list incl. 4n multiply, OpenMP {threads} threads) on the multiset of the GPU's "
+                      f"timed proofs: {med:.2f} s/proof "
                       f"(min {times[0]:.2f}, max {times[-1]:.2f})" + ("" if k >= 3 else f"; capped at {max_seconds:.0f} s")}

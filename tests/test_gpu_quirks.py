@@ -359,3 +359,56 @@ def test_quirks_mode_group_ordinary_inputs(K, monkeypatch):
     got = group_outcome(K, "grandsum", ptau, Fs, Ts, sF, sT, 4)
     monkeypatch.setenv("KGS_REFERENCE_QUIRKS", "0")
     assert got == gpu_outcome(K, "grandsum", ptau, Fs, Ts, sF, sT)
+
+
+def test_replay_failure_on_one_rank_aborts_the_group(K, monkeypatch):
+    """a failure of the quirks replay that happens on ONE rank only (here an
+    injected out-of-memory in rank 2's gather buffers, KGS_DEBUG_ALLOC_RANK) is not a decision every
+    rank shares: that rank aborts the group and the others fail at once with "rank group aborted",
+    instead of waiting in their next all-gather for the group timeout (120 s)."""
+    import threading
+    import time
+    monkeypatch.setenv("KGS_REFERENCE_QUIRKS", "1")
+    ptau = common.oracle_ptau(9)
+    world, nbits = 4, 5
+    ordinary = common.make_inputs(321, nbits, 1, False)
+    degenerate = inputs("x", nbits, 1, False)  # operands of degree 1: the replay runs
+    g = K.Group.local(world)
+    ctxs = [K.Context(0) for _ in range(world)]
+    for r, c in enumerate(ctxs):
+        c.load_ptau(ptau, nbits)
+        c.set_group(g, r)
+
+    def run_all(Fs, Ts):
+        outs = [None] * world
+
+        def run(r):
+            try:
+                outs[r] = ctxs[r].prove(K.GRANDSUM, nbits, Fs, Ts, None, None, mont_out=False)[:2]
+            except K.KgsError as e:
+                outs[r] = e
+        th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=300)
+        return outs
+
+    warm = run_all(*ordinary[:2])  # every pool buffer of this shape exists afterwards
+    assert not any(isinstance(o, Exception) for o in warm), warm
+    monkeypatch.setenv("KGS_DEBUG_ALLOC_LIMIT", "64")
+    monkeypatch.setenv("KGS_DEBUG_ALLOC_RANK", "2")
+    t0 = time.monotonic()
+    outs = run_all(*degenerate[:2])
+    dt = time.monotonic() - t0
+    monkeypatch.delenv("KGS_DEBUG_ALLOC_LIMIT")
+    monkeypatch.delenv("KGS_DEBUG_ALLOC_RANK")
+    assert all(isinstance(o, K.KgsError) for o in outs), outs
+    assert "out of memory" in str(outs[2]).lower(), outs[2]
+    for r in (0, 1, 3):
+        assert "aborted" in str(outs[r]), (r, outs[r])
+    assert dt < 60, f"the other ranks waited {dt:.1f} s"
+    for c in ctxs:
+        c.set_group(None)
+        c.close()
+    g.close()
