@@ -501,5 +501,8 @@ struct CopyJob {
   size_t len;
 };
 void par_copy(const std::vector<CopyJob>& jobs);
+// one vector into pinned staging; ready(offset, len) on the calling thread per `dma`-byte span, in
+// order, once that span is copied (prover.cpp)
+void stream_copy(uint8_t* dst, const uint8_t* src, size_t len, size_t dma, const std::function<void(size_t, size_t)>& ready);
 
 }  // namespace kgsi

@@ -28,6 +28,7 @@
 #include <functional>
 #include <atomic>
 #include <thread>
+#include <immintrin.h>
 #include <vector>
 
 #include "../../include/kgs.h"
@@ -1408,26 +1409,65 @@ static unsigned copy_threads() {
   return n;
 }
 namespace {
-// Invariants (DESIGN.md §5 "Round 6: the round-5 fault"): a piece is claimed exactly once, before
-// par_copy returns, and pool threads make no HIP call (every DMA is enqueued by the thread that owns
-// the call, after par_copy returned). Queue entries outlive their task (a helper that wakes late pops a
+// 16 B non-temporal stores: the staging copy writes 32 MiB that the CPU never reads back, so the
+// stores bypass the caches (no read-for-ownership of the destination lines). Measured on the GPU
+// box's host (profiles/ubench/host_copy_bw.cpp, profiles/r06/host_copy_bw.txt): one 32 MiB vector
+// into pinned staging in 0.26 ms with 4 threads (130 GB/s) against 0.44 ms for memcpy. The sfence
+// makes the lines globally visible before the piece is counted done, i.e. before its DMA is enqueued.
+void copy_nt(uint8_t* d, const uint8_t* s, size_t n) {
+  static const bool plain = [] {  // KGS_COPY_NT=0: memcpy (A/B)
+    const char* e = getenv("KGS_COPY_NT");
+    return e && e[0] == '0';
+  }();
+  if (plain) {
+    memcpy(d, s, n);
+    return;
+  }
+  size_t i = 0;
+  const size_t head = (16 - ((uintptr_t)d & 15)) & 15;
+  if (head) {
+    const size_t h = std::min(head, n);
+    memcpy(d, s, h);
+    i = h;
+  }
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128((const __m128i*)(s + i)), b = _mm_loadu_si128((const __m128i*)(s + i + 16));
+    const __m128i c = _mm_loadu_si128((const __m128i*)(s + i + 32)), e = _mm_loadu_si128((const __m128i*)(s + i + 48));
+    _mm_stream_si128((__m128i*)(d + i), a);
+    _mm_stream_si128((__m128i*)(d + i + 16), b);
+    _mm_stream_si128((__m128i*)(d + i + 32), c);
+    _mm_stream_si128((__m128i*)(d + i + 48), e);
+  }
+  if (i < n) memcpy(d + i, s + i, n - i);
+  _mm_sfence();
+}
+
+// Invariants (DESIGN.md §13 "The round-5 illegal-address fault"): a piece is claimed exactly once,
+// before par_copy / stream_copy returns, and pool threads make no HIP call (every DMA is enqueued by
+// the thread that owns the call). Queue entries outlive their task (a helper that wakes late pops a
 // finished task): such a late `work()` must claim nothing, which `closed` checks.
 struct CopyTask {
   std::vector<CopyJob> pieces;
   std::atomic<size_t> next{0}, done{0};
-  std::atomic<bool> closed{false};  // set once par_copy has seen every piece done
+  std::atomic<bool> closed{false};  // set once the owner has seen every piece done
+  // stream_copy: pieces left to copy per DMA piece (piece i belongs to DMA piece i / per_dma)
+  std::unique_ptr<std::atomic<uint32_t>[]> left;
+  size_t per_dma = 0;
   std::mutex mu;
   std::condition_variable cv;
-  void work() {
-    size_t i, mine = 0;
-    while ((i = next.fetch_add(1)) < pieces.size()) {
-      if (closed.load(std::memory_order_acquire)) {
-        fprintf(stderr, "kgs: copy piece %zu claimed after its task completed\n", i);
-        abort();
-      }
-      memcpy(pieces[i].dst, pieces[i].src, pieces[i].len);
-      mine++;
+  bool copy_one(size_t i) {  // false: nothing left to claim
+    if (i >= pieces.size()) return false;
+    if (closed.load(std::memory_order_acquire)) {
+      fprintf(stderr, "kgs: copy piece %zu claimed after its task completed\n", i);
+      abort();
     }
+    copy_nt(pieces[i].dst, pieces[i].src, pieces[i].len);
+    if (left) left[i / per_dma].fetch_sub(1, std::memory_order_release);
+    return true;
+  }
+  void work() {
+    size_t mine = 0;
+    while (copy_one(next.fetch_add(1))) mine++;
     if (mine && done.fetch_add(mine) + mine == pieces.size()) {
       std::lock_guard<std::mutex> lk(mu);
       cv.notify_all();
@@ -1458,6 +1498,35 @@ struct CopyPool {  // leaked on purpose: its detached threads outlive static des
     return *p;
   }
 };
+struct Active {  // copies running at once in the process: they share the copy threads
+  int n;
+  Active() : n(g_copy_active.fetch_add(1) + 1) {}
+  ~Active() { g_copy_active.fetch_sub(1); }
+};
+// threads (this one included) for one copy: KGS_COPY_TASK_THREADS (default 2), within the share of
+// the copy threads left by the other copies running. The host copy bandwidth of the GPU box peaks at
+// 2-4 threads (profiles/r06/host_copy_bw.txt), but the proof does not get faster with it: F_0's DMA,
+// not its copy, sets its arrival. Same-box A/Bs (profiles/r06/copy_ab*, f0_ab): single-proof median
+// 14.43 ms with 2 threads, 14.82 with 4, 14.54 for round 5's span-by-span copy; in flight all within
+// the run-to-run spread (87.7-90.8 proofs/s against 92.7-93.1 device-resident)
+unsigned task_threads(const Active& a, size_t pieces) {
+  static const unsigned per = [] {
+    const char* e = getenv("KGS_COPY_TASK_THREADS");
+    const int v = e ? atoi(e) : 2;
+    return (unsigned)(v >= 1 && v <= 64 ? v : 2);
+  }();
+  unsigned nth = std::min(per, std::max(1u, copy_threads() / (unsigned)std::max(1, a.n)));
+  return std::max(1u, std::min<unsigned>(nth, (unsigned)pieces));
+}
+void start_helpers(const std::shared_ptr<CopyTask>& task, unsigned nth) {
+  if (nth <= 1) return;
+  CopyPool& pool = CopyPool::get();
+  {
+    std::lock_guard<std::mutex> lk(pool.mu);
+    for (unsigned t = 1; t < nth; t++) pool.q.push_back(task);  // helpers; the calling thread is the nth
+  }
+  pool.cv.notify_all();
+}
 }  // namespace
 
 void par_copy(const std::vector<CopyJob>& jobs) {
@@ -1465,26 +1534,59 @@ void par_copy(const std::vector<CopyJob>& jobs) {
   auto task = std::make_shared<CopyTask>();
   for (const auto& j : jobs)
     for (size_t o = 0; o < j.len; o += piece) task->pieces.push_back({j.dst + o, j.src + o, std::min(piece, j.len - o)});
-  struct Active {
-    int n;
-    Active() : n(g_copy_active.fetch_add(1) + 1) {}
-    ~Active() { g_copy_active.fetch_sub(1); }
-  } active;
-  unsigned nth = std::thread::hardware_concurrency();
-  nth = std::max(1u, std::min(nth, copy_threads()) / (unsigned)std::max(1, active.n));
-  nth = std::min<unsigned>(nth, (unsigned)task->pieces.size());
-  if (nth > 1) {
-    CopyPool& pool = CopyPool::get();
-    {
-      std::lock_guard<std::mutex> lk(pool.mu);
-      for (unsigned t = 1; t < nth; t++) pool.q.push_back(task);  // helpers; this thread is the nth
-    }
-    pool.cv.notify_all();
-  }
+  Active active;
+  start_helpers(task, task_threads(active, task->pieces.size()));
   task->work();
   std::unique_lock<std::mutex> lk(task->mu);
   task->cv.wait(lk, [&] { return task->done.load() == task->pieces.size(); });
   task->closed.store(true, std::memory_order_release);
+}
+
+// One vector into pinned staging, copied in 256 KiB pieces claimed in address order by this thread
+// and the pool's helpers; `ready(offset, len)` runs on THIS thread for each `dma`-byte span, in order,
+// as soon as every piece of it is copied (it enqueues that span's DMA). So the first DMA starts after
+// one span's copy and the link is fed while the rest is still being copied, at the copy bandwidth of
+// several threads (round 5 copied span by span with two threads each, ~1.2 ms for a 32 MiB vector).
+// An exception from `ready` is held until every piece is copied (helpers never outlive the call's
+// writes into the staging), then rethrown; later spans are not enqueued.
+void stream_copy(uint8_t* dst, const uint8_t* src, size_t len, size_t dma, const std::function<void(size_t, size_t)>& ready) {
+  const size_t sub = (size_t)256 << 10;
+  dma = std::max(sub, dma / sub * sub);
+  auto task = std::make_shared<CopyTask>();
+  for (size_t o = 0; o < len; o += sub) task->pieces.push_back({dst + o, src + o, std::min(sub, len - o)});
+  const size_t ndma = (len + dma - 1) / dma;
+  task->per_dma = dma / sub;
+  task->left.reset(new std::atomic<uint32_t>[ndma]);
+  for (size_t k = 0; k < ndma; k++)
+    task->left[k].store((uint32_t)std::min(task->per_dma, task->pieces.size() - k * task->per_dma));
+  Active active;
+  start_helpers(task, task_threads(active, task->pieces.size()));
+  size_t issued = 0, mine = 0;
+  std::exception_ptr err;
+  auto flush = [&] {
+    while (issued < ndma && task->left[issued].load(std::memory_order_acquire) == 0) {
+      const size_t o = issued * dma;
+      if (!err) {
+        try {
+          ready(o, std::min(dma, len - o));
+        } catch (...) {
+          err = std::current_exception();
+        }
+      }
+      issued++;
+    }
+  };
+  while (task->copy_one(task->next.fetch_add(1))) {
+    mine++;
+    flush();
+  }
+  if (mine) task->done.fetch_add(mine);
+  while (issued < ndma) {  // the helpers' last pieces (each at most one 256 KiB copy away)
+    flush();
+    if (issued < ndma) _mm_pause();
+  }
+  task->closed.store(true, std::memory_order_release);
+  if (err) std::rethrow_exception(err);
 }
 
 // Caller buffers the DMAs can read / write in place: memory the caller already pinned (hipHostMalloc,
@@ -1657,13 +1759,28 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   // Vector 0 (F_0, whose transform starts round 1) in 2 MiB pieces, so that its first DMA starts
   // ~0.03 ms into the call and its last ends ~0.04 ms after its copy; the others in 8 MiB pieces
   // (fewer DMA submissions on the feeder thread)
+  static const bool span_copy = [] {  // KGS_STREAM_COPY=0: round 5's span-by-span copy (A/B)
+    const char* e = getenv("KGS_STREAM_COPY");
+    return e && e[0] == '0';
+  }();
   auto feed = [&](size_t v, hipStream_t st) {
-    const size_t piece = (size_t)(v == 0 ? 2 : 8) << 20;
-    for (size_t o = 0; o < E; o += piece) {
-      const size_t len = std::min(piece, E - o);
-      par_copy({{in_jobs[v].dst + o, in_jobs[v].src + o, len}});
-      HC(hipMemcpyAsync((uint8_t*)dsts[v] + o, in_jobs[v].dst + o, len, hipMemcpyHostToDevice, st));
+    static const size_t f0_span = [] {  // KGS_F0_SPAN_MB: DMA span of vector 0 (A/B; default 2 MiB)
+      const char* e = getenv("KGS_F0_SPAN_MB");
+      const int v = e ? atoi(e) : 2;
+      return (size_t)(v >= 1 && v <= 64 ? v : 2) << 20;
+    }();
+    const size_t span = v == 0 ? f0_span : (size_t)8 << 20;
+    if (span_copy) {
+      for (size_t o = 0; o < E; o += span) {
+        const size_t len = std::min(span, E - o);
+        par_copy({{in_jobs[v].dst + o, in_jobs[v].src + o, len}});
+        HC(hipMemcpyAsync((uint8_t*)dsts[v] + o, in_jobs[v].dst + o, len, hipMemcpyHostToDevice, st));
+      }
+      return;
     }
+    stream_copy(in_jobs[v].dst, in_jobs[v].src, E, span, [&](size_t o, size_t len) {
+      HC(hipMemcpyAsync((uint8_t*)dsts[v] + o, in_jobs[v].dst + o, len, hipMemcpyHostToDevice, st));
+    });
   };
   // declared before the feeder: destroyed after it is joined, so streams are drained and buffers
   // unpinned only once nothing can enqueue another DMA on them
@@ -1716,7 +1833,28 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
       ctx->ev_in.push_back(e);
     }
     in.ready.assign(in_jobs.size(), nullptr);
-    feed(0, ctx->st);
+    // KGS_F0_STREAM=copy (A/B): F_0's DMAs on the copy stream too, the main stream waits on ev_in[0]
+    static const bool f0_on_copy = [] {
+      const char* e = getenv("KGS_F0_STREAM");
+      return e && !strcmp(e, "copy");
+    }();
+    if (f0_on_copy) {
+      feed(0, ctx->st_copy);
+      HC(hipEventRecord(ctx->ev_in[0], ctx->st_copy));
+      in.ready[0] = ctx->ev_in[0];
+    } else {
+      feed(0, ctx->st);
+    }
+    // the link carries F_0 first: the copy stream's DMAs start after F_0's last one (ev_in[0] on the
+    // main stream, which holds only F_0's DMAs here). With the multi-threaded staging copy, T_0's DMAs
+    // otherwise shared the link with F_0's and F_0 arrived ~0.5 ms later (profiles/r06/copy_ab/);
+    // KGS_FEED_ORDER=0 lets them overlap (A/B)
+    static const bool ordered = [] {
+      const char* e = getenv("KGS_FEED_ORDER");
+      return !(e && e[0] == '0');
+    }();
+    const bool wait_f0 = ordered && in_jobs.size() > 1 && !f0_on_copy;  // (same stream: ordered anyway)
+    if (wait_f0) HC(hipEventRecord(ctx->ev_in[0], ctx->st));
     for (size_t v = 1; v < in_jobs.size(); v++) in.ready[v] = ctx->ev_in[v];
     // vectors 1.. are copied into their pinned slots and DMA'd by a feeder thread while the prover
     // already enqueues (and the GPU runs) vector 0's work; prove_impl waits for a vector's DMA to be
@@ -1725,6 +1863,7 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
       feeder.t = std::thread([&, dev = ctx->device] {
         try {
           HC(hipSetDevice(dev));
+          if (wait_f0) HC(hipStreamWaitEvent(ctx->st_copy, ctx->ev_in[0], 0));
           for (size_t v = 1; v < in_jobs.size(); v++) {
             feed(v, ctx->st_copy);
             HC(hipEventRecord(ctx->ev_in[v], ctx->st_copy));

@@ -114,6 +114,82 @@ __global__ void __launch_bounds__(256) k_batch(uint32_t* io, int iters) {
   io[16 * tid] = o;
 }
 
+// Round 6 (VERDICT r5 Next #4): the CROSS-LANE wave batch. K chains per lane whose pending state
+// (accumulator X, Y and the forward prefix products) lives in LDS; per step ONE inversion per wave:
+// each lane's K-chain product t_l, an inclusive and an exclusive-suffix product scan of t_l over the
+// 64 lanes (shuffles, 6 levels each), the wave total inverted once, 1/t_l = inv * prefix_excl *
+// suffix_excl, then each lane's backward pass and affine adds. Fq products per entry:
+//   forward 1 + backward 2 + affine add 3 (lambda, lambda^2, lambda * (x1 - x3)) = 6 per entry,
+//   + (12 scan + 2 + inversion) per lane per step = (14 + INV) / K per entry,
+// INV = 253 squarings + 120 multiplies (q - 2 has 121 set bits) = 373 products by the whole wave.
+__device__ __forceinline__ fq29 shfl_fq29(const fq29& a, int src_lane) {
+  fq29 r;
+#pragma unroll
+  for (int j = 0; j < 9; j++) r.l[j] = __shfl(a.l[j], src_lane);
+  return r;
+}
+
+template <int K>
+__global__ void __launch_bounds__(64) k_xlane(uint32_t* io, int iters) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x;
+  __shared__ fq29 sX[K][64], sY[K][64], sP[K][64];
+  const fq29 px = load29(io + 16 * tid), py = load29(io + 16 * tid + 8);
+#pragma unroll
+  for (int i = 0; i < K; i++) {
+    fq29 x = px;
+    x.l[1] += i + 1;
+    sX[i][lane] = x;
+    sY[i][lane] = py;
+  }
+  const fq29 one = fq29::from(f29::ONE);
+  for (int it = 0; it < iters; it++) {
+    fq29 acc = one;
+    for (int i = 0; i < K; i++) {  // forward: prefix products of this lane's K differences
+      fq29 x2 = px;
+      x2.l[0] += it + 3 * i;
+      const fq29 d = fq29::sub<64, 1>(x2, sX[i][lane]).norm();
+      sP[i][lane] = acc;
+      acc = fq29::mul(acc, d);
+    }
+    // inclusive prefix and exclusive suffix products of the lane totals over the wave
+    fq29 pre = acc, suf = one;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const fq29 y = shfl_fq29(pre, lane >= off ? lane - off : lane);
+      if (lane >= off) pre = fq29::mul(pre, y);
+    }
+    fq29 sacc = acc;  // inclusive suffix
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const fq29 y = shfl_fq29(sacc, lane + off < 64 ? lane + off : lane);
+      if (lane + off < 64) sacc = fq29::mul(sacc, y);
+    }
+    const fq29 pre_ex = lane ? shfl_fq29(pre, lane - 1) : one;
+    const fq29 pre_excl = lane ? pre_ex : one;
+    suf = shfl_fq29(sacc, lane < 63 ? lane + 1 : lane);
+    if (lane == 63) suf = one;
+    const fq29 total = shfl_fq29(pre, 63);
+    fq29 inv = inv_fermat(total);                                  // one inversion per wave
+    inv = fq29::mul(fq29::mul(inv, pre_excl), suf);                // 1 / (this lane's K-product)
+    for (int i = K - 1; i >= 0; i--) {  // backward pass + affine adds
+      fq29 x2 = px, y2 = py;
+      x2.l[0] += it + 3 * i;
+      y2.l[2] += it;
+      const fq29 X = sX[i][lane], Y = sY[i][lane];
+      const fq29 d = fq29::sub<64, 1>(x2, X).norm();
+      const fq29 inv_i = fq29::mul(inv, sP[i][lane]);
+      inv = fq29::mul(inv, d);
+      const fq29 lam = fq29::mul(fq29::sub<64, 1>(y2, Y).norm(), inv_i);
+      const fq29 x3 = fq29::sub<128, 2>(fq29::sqr(lam), fq29::add(X, x2)).norm();
+      sY[i][lane] = fq29::sub<64, 1>(fq29::mul(lam, fq29::sub<64, 1>(X, x3).norm()), Y).norm();
+      sX[i][lane] = x3;
+    }
+  }
+  uint32_t o = 0;
+  for (int i = 0; i < K; i++) o ^= sX[i][lane].l[0] ^ sY[i][lane].l[3];
+  io[16 * tid] = o;
+}
+
 // production XYZZ mixed add in the same harness (as madd29.hip)
 __global__ void __launch_bounds__(256) k_xyzz(uint32_t* io, int iters) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -186,6 +262,12 @@ int main() {
   BA(2, 0, "batch-affine K=2, Fermat")
   BA(4, 0, "batch-affine K=4, Fermat")
   BA(8, 0, "batch-affine K=8, Fermat")
+#define XL(KK, name)                                                                                          \
+  if (timed([&] { hipLaunchKernelGGL((k_xlane<KK>), dim3(blocks * 4), dim3(64), 0, 0, d, iters); },            \
+            threads * KK * iters, name, "adds")) return 1;
+  XL(8, "cross-lane wave batch K=8, Fermat")
+  XL(16, "cross-lane wave batch K=16, Fermat")
+  // K = 32 does not compile: 3 x 32 x 64 x 36 B = 221 KB of pending state exceeds the CU's 160 KB LDS
   BA(2, 1, "batch-affine K=2, binary Euclid")
   BA(4, 1, "batch-affine K=4, binary Euclid")
   BA(8, 1, "batch-affine K=8, binary Euclid")
