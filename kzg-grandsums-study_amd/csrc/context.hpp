@@ -76,7 +76,7 @@ hipError_t dev_malloc(void** p, size_t bytes);
 constexpr int KGS_MAX_POLS = 1024;
 
 #ifndef KGS_C_MAX
-#define KGS_C_MAX 17
+#define KGS_C_MAX 20
 #endif
 
 struct DBuf {

@@ -46,14 +46,24 @@ struct MsmTables {
 };
 
 constexpr int MSM_SL_G_MAX = 128;  // chunks per partition the lo-pass count buffer holds (msm.hip SL_G)
+// Bucket sort of an MSM with window c (msm.hip): LOB low bits of key - 1 are sorted inside a partition
+// (<= 8: the lo pass keeps them in a byte), the other c - 1 - LOB bits select one of NH = 2^(c-1-LOB)
+// partitions: 256 for 16 <= c <= 17, 512 / 1024 / 2048 for c = 18 / 19 / 20
+constexpr int MSM_NH_MAX = 2048;
+inline int msm_lob(int c) {
+  int lob = c - 1 < 7 ? c - 1 : 7;
+  if (c - 9 > lob) lob = c - 9 > 8 ? 8 : c - 9;
+  return lob;
+}
+inline int msm_nh(int c) { return (1 << (c - 1)) >> msm_lob(c); }
 struct MsmWork {
   int32_t* digit = nullptr;  // reused as the partition-pass value array
   uint8_t* lo = nullptr;
-  uint32_t* blockhist = nullptr;  // (NH <= 264) x ceil(N/256) per-block partition counts
+  uint32_t* blockhist = nullptr;  // NH x ceil(N / (256 * SORT_SPT)) per-block partition counts
   uint32_t *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *sorted = nullptr;
   uint32_t* part = nullptr;      // bucket row + column sums (2^h + 2^l run records, msm.hip k_rowcol)
   uint32_t* segowner = nullptr;  // bucket of each segment's first run
-  uint32_t* locnt = nullptr;     // lo pass: 256 partitions x 256 lo x MSM_SL_G_MAX chunks counts / bases
+  uint32_t* locnt = nullptr;     // lo pass: NH partitions x 256 lo x MSM_SL_G_MAX chunks counts / bases
   uint32_t* chunklist = nullptr; // combine levels: 3 lists of chunk-start segments
   uint32_t* chunkcnt = nullptr;  // their lengths
   uint32_t* raw29 = nullptr;     // accumulate output in the fq29 form (B + 1 + nseg entries x 160 B)

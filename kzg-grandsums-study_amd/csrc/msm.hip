@@ -19,6 +19,7 @@
 namespace kgs {
 
 static inline unsigned nb(uint64_t work, unsigned bs = 256) { return (unsigned)((work + bs - 1) / bs); }
+constexpr int NH_MAX = MSM_NH_MAX;  // bucket-sort partitions (kernels.hpp msm_lob)
 
 // ------------------------------------------------------------------ window table precompute
 __global__ void __launch_bounds__(256) k_tab_dbl(uint32_t* __restrict__ tmp, const uint32_t* __restrict__ prev,
@@ -92,7 +93,8 @@ void msm_build_table(hipStream_t st, uint32_t* table, uint64_t npts, int c, int 
 // Entry (j, i) = (window, point) with signed digit d = digit_j(from_mont(scalar_i)); key |d| in
 // [0, B], B = 2^(c-1); key 0 entries are dropped. Sort by key without global per-entry atomics:
 //  sorting is by k' = key - 1 in [0, B) (c - 1 bits): pass 1 partitions by p = k' >> LOB
-//          (NH = B >> LOB <= 256 partitions of 2^LOB keys each). Per-block partition counts come from a histogram pass whose
+//          (NH = B >> LOB <= NH_MAX = 2048 partitions of 2^LOB <= 256 keys each; NH = 256 up to c = 17,
+//          2^(c-9) above: c = 20 has 2048). Per-block partition counts come from a histogram pass whose
 //          block x partition table is scanned; each block then counting-sorts its entries in LDS
 //          and writes them out as contiguous per-partition runs (coalesced stores instead of one
 //          scattered 4 B + 1 B store per entry). Digits are RECOMPUTED from the scalars in both
@@ -149,6 +151,34 @@ __device__ __forceinline__ uint32_t wave_excl_scan256(const uint32_t* a, uint32_
   return __shfl(incl, 63);  // total
 }
 
+// exclusive scan of a[0..n) by all NT threads of the block (n <= NH_MAX: up to 8 elements per thread
+// at NT = 256); tmp: NT words of LDS; out may alias a; ends with a barrier; returns the total
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan(const uint32_t* a, uint32_t* out, int n, uint32_t* tmp) {
+  const int t = threadIdx.x;
+  const int per = (n + NT - 1) / NT;
+  const int lo = t * per < n ? t * per : n, hi = lo + per < n ? lo + per : n;
+  uint32_t sum = 0;
+  for (int i = lo; i < hi; i++) sum += a[i];
+  tmp[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < NT; off <<= 1) {
+    const uint32_t v = t >= off ? tmp[t - off] : 0u;
+    __syncthreads();
+    tmp[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = t ? tmp[t - 1] : 0u;
+  const uint32_t total = tmp[NT - 1];
+  for (int i = lo; i < hi; i++) {
+    const uint32_t v = a[i];
+    out[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  return total;
+}
+
 // partition of a nonzero digit magnitude: (key - 1) >> lob
 __device__ __forceinline__ uint32_t part_of(uint32_t key, int lob) { return (key - 1) >> lob; }
 
@@ -164,8 +194,8 @@ __global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ bh, co
   KGS_AUX_PRIO();
   // per-block partition histogram, stored transposed: bh[p * nblk + block]
   constexpr int W = (255 + C - 1) / C;
-  __shared__ uint32_t h[256];
-  h[threadIdx.x] = 0;
+  __shared__ uint32_t h[NH_MAX];
+  for (int t = threadIdx.x; t < NH; t += 256) h[t] = 0;
   __syncthreads();
   for (int q = 0; q < SORT_SPT; q++) {
     const uint64_t i = ((uint64_t)blockIdx.x * SORT_SPT + q) * 256 + threadIdx.x;
@@ -179,7 +209,7 @@ __global__ void __launch_bounds__(256) k_sort_hist(uint32_t* __restrict__ bh, co
     }
   }
   __syncthreads();
-  if ((int)threadIdx.x < NH) bh[(uint64_t)threadIdx.x * nblk + blockIdx.x] = h[threadIdx.x];
+  for (int t = threadIdx.x; t < NH; t += 256) bh[(uint64_t)t * nblk + blockIdx.x] = h[t];
 }
 
 // grid = NH workgroups: exclusive scan of one partition's per-block counts (in place) and its total
@@ -211,17 +241,22 @@ __global__ void __launch_bounds__(256) k_sort_scan_blocks(uint32_t* __restrict__
 
 __device__ __forceinline__ uint32_t chunk_count(uint32_t size);
 
-// hi_off[p] = exclusive scan of partition totals (NH <= 256); offsets[B+1] = total; cpre = exclusive
-// scan of the lo pass's chunks per partition (cpre[NH] = all chunks)
-__global__ void __launch_bounds__(64) k_sort_scan(uint32_t* __restrict__ hi_off, const uint32_t* __restrict__ ptot,
-                                                  int NH, uint32_t* __restrict__ offsets, uint32_t B,
-                                                  uint32_t* __restrict__ cpre) {
+// hi_off[p] = exclusive scan of partition totals (NH <= NH_MAX); offsets[B+1] = total; cpre = exclusive
+// scan of the lo pass's chunks per partition (cpre[NH] = all chunks); bpart[b] = the partition of
+// lo-pass block b (its chunk is b - cpre[bpart[b]])
+__global__ void __launch_bounds__(256) k_sort_scan(uint32_t* __restrict__ hi_off, const uint32_t* __restrict__ ptot,
+                                                   int NH, uint32_t* __restrict__ offsets, uint32_t B,
+                                                   uint32_t* __restrict__ cpre, uint32_t* __restrict__ bpart) {
   KGS_AUX_PRIO();
-  __shared__ uint32_t gp[256];
-  const uint32_t total = wave_excl_scan256(ptot, hi_off, NH);
-  for (int q = threadIdx.x; q < NH; q += 64) gp[q] = chunk_count(ptot[q]);
+  __shared__ uint32_t gp[NH_MAX], tmp[256];
+  const uint32_t total = block_excl_scan<256>(ptot, hi_off, NH, tmp);
+  for (int q = threadIdx.x; q < NH; q += 256) gp[q] = chunk_count(ptot[q]);
   __syncthreads();
-  const uint32_t chunks = wave_excl_scan256(gp, cpre, NH);
+  const uint32_t chunks = block_excl_scan<256>(gp, cpre, NH, tmp);
+  for (int q = threadIdx.x; q < NH; q += 256) {
+    const uint32_t b0 = cpre[q];
+    for (uint32_t g = 0; g < gp[q]; g++) bpart[b0 + g] = (uint32_t)q;
+  }
   if (threadIdx.x == 0) {
     hi_off[NH] = total;
     cpre[NH] = chunks;
@@ -230,7 +265,8 @@ __global__ void __launch_bounds__(64) k_sort_scan(uint32_t* __restrict__ hi_off,
   }
 }
 
-// dynamic LDS: 256 * W * (4 + 2) bytes of staging
+// dynamic LDS (part_lds in msm_run): NS = 256 * SORT_SPT * W staged entries (4 B value, 2 B partition,
+// 1 B lo) and the block's per-partition base / offset / cursor (3 x NH words)
 // scalar i multiplies SRS point pbase + pstride * i (a contiguous or strided slice of the SRS)
 template <int C>
 __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, uint8_t* __restrict__ tlo,
@@ -241,24 +277,24 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
   KGS_AUX_PRIO();
   constexpr int W = (255 + C - 1) / C;
   extern __shared__ uint32_t smem[];
-  uint32_t* sval = smem;                                        // 256 * SORT_SPT * W
-  uint16_t* skey = (uint16_t*)(smem + 256 * SORT_SPT * W);      // same count (key - 1 < 2^16)
-  __shared__ uint32_t base[256], loff[256], cur[256];
-  __shared__ uint32_t total;
+  constexpr int NS = 256 * SORT_SPT * W;
+  uint32_t* sval = smem;                          // NS values
+  uint32_t* base = smem + NS;                     // NH each
+  uint32_t* loff = base + NH;
+  uint32_t* cur = loff + NH;
+  uint16_t* spart = (uint16_t*)(cur + NH);        // NS partitions (< NH_MAX)
+  uint8_t* slo = (uint8_t*)(spart + NS);          // NS lo keys (< 2^LOB <= 256)
+  __shared__ uint32_t tmp[256];
   const uint32_t blk = blockIdx.x, tid = threadIdx.x;
-  if ((int)tid < NH) {
-    const uint32_t mine = bh[(uint64_t)tid * nblk + blk];
-    const uint32_t nxt = blk + 1 < nblk ? bh[(uint64_t)tid * nblk + blk + 1] : ptot[tid];
-    base[tid] = hi_off[tid] + mine;
-    cur[tid] = nxt - mine;  // this block's count, scanned below
+  for (int t = tid; t < NH; t += 256) {
+    const uint32_t mine = bh[(uint64_t)t * nblk + blk];
+    const uint32_t nxt = blk + 1 < nblk ? bh[(uint64_t)t * nblk + blk + 1] : ptot[t];
+    base[t] = hi_off[t] + mine;
+    cur[t] = nxt - mine;  // this block's count, scanned below
   }
   __syncthreads();
-  if (tid < 64) {
-    const uint32_t t = wave_excl_scan256(cur, loff, NH);
-    if (tid == 0) total = t;
-  }
-  __syncthreads();
-  if ((int)tid < NH) cur[tid] = loff[tid];
+  const uint32_t tot = block_excl_scan<256>(cur, loff, NH, tmp);
+  for (int t = tid; t < NH; t += 256) cur[t] = loff[t];
   __syncthreads();
   for (int q = 0; q < SORT_SPT; q++) {
     const uint64_t i = ((uint64_t)blk * SORT_SPT + q) * 256 + tid;
@@ -271,20 +307,20 @@ __global__ void __launch_bounds__(256) k_sort_part(uint32_t* __restrict__ tval, 
       for (int j = 0; j < W; j++) {
         if (!d[j]) continue;
         const uint32_t k = (uint32_t)(d[j] < 0 ? -d[j] : d[j]);
-        const uint32_t pos = atomicAdd(&cur[part_of(k, lob)], 1u);
+        const uint32_t p = part_of(k, lob);
+        const uint32_t pos = atomicAdd(&cur[p], 1u);
         sval[pos] = ((uint32_t)j * (uint32_t)Nsrs + pidx) | (d[j] < 0 ? 0x80000000u : 0u);
-        skey[pos] = (uint16_t)(k - 1);
+        spart[pos] = (uint16_t)p;
+        slo[pos] = (uint8_t)((k - 1) - (p << lob));
       }
     }
   }
   __syncthreads();
-  const uint32_t tot = total;
   for (uint32_t e = tid; e < tot; e += 256) {
-    const uint32_t k = skey[e];  // key - 1
-    const uint32_t p = k >> lob;
+    const uint32_t p = spart[e];
     const uint32_t g = base[p] + (e - loff[p]);
     tval[g] = sval[e];
-    tlo[g] = (uint8_t)(k - (p << lob));
+    tlo[g] = slo[e];
   }
 }
 
@@ -330,30 +366,22 @@ __device__ __forceinline__ uint32_t chunk_count(uint32_t size) {
 }
 
 // The lo-pass kernels run one workgroup per (partition, chunk) on a 1-D grid: cpre[p] = chunks of
-// the partitions before p (k_sort_scan), block b belongs to the partition p with
+// the partitions before p (k_sort_scan), block b belongs to the partition p = bpart[b] with
 // cpre[p] <= b < cpre[p + 1]; blocks past cpre[NH] (the host sizes the grid by an upper bound) exit.
-// (p, g, G) of block b with one global round trip: the block stages cpre and hi_off (NH + 1 words each) in LDS
-// and searches there (the 8 dependent L2 loads of a global binary search cost microseconds per block);
-// also returns the partition's range [s0, s1). Called by every thread of the block.
-__device__ __forceinline__ bool chunk_of_block_lds(const uint32_t* __restrict__ cpre, const uint32_t* __restrict__ hi_off,
-                                                   int NH, uint32_t b, uint32_t* scp, uint32_t* shi, uint32_t& p,
-                                                   uint32_t& g, uint32_t& G, uint32_t& s0, uint32_t& s1) {
-  for (uint32_t t = threadIdx.x; t <= (uint32_t)NH; t += blockDim.x) {
-    scp[t] = cpre[t];
-    shi[t] = hi_off[t];
-  }
-  __syncthreads();
-  if (b >= scp[NH]) return false;
-  uint32_t lo = 0, hi = (uint32_t)NH;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (scp[mid] <= b) lo = mid; else hi = mid;
-  }
-  p = lo;
-  g = b - scp[lo];
-  G = scp[lo + 1] - scp[lo];
-  s0 = shi[lo];
-  s1 = shi[lo + 1];
+// (p, g, G) of block b and the partition's range [s0, s1) in two dependent rounds of loads (the table
+// bpart replaces round 3's LDS copy of cpre / hi_off and its binary search, which at up to 2048
+// partitions would take 16 KB of LDS per block). Uniform per block.
+__device__ __forceinline__ bool chunk_of_block(const uint32_t* __restrict__ cpre, const uint32_t* __restrict__ hi_off,
+                                               const uint32_t* __restrict__ bpart, int NH, uint32_t b, uint32_t& p,
+                                               uint32_t& g, uint32_t& G, uint32_t& s0, uint32_t& s1) {
+  const uint32_t nchunks = cpre[NH];
+  if (b >= nchunks) return false;
+  p = bpart[b];
+  const uint32_t c0 = cpre[p], c1 = cpre[p + 1];
+  g = b - c0;
+  G = c1 - c0;
+  s0 = hi_off[p];
+  s1 = hi_off[p + 1];
   return true;
 }
 
@@ -369,12 +397,12 @@ __device__ __forceinline__ void chunk_range(uint32_t s0, uint32_t s1, uint32_t G
 // sub-histogram per wave against LDS atomic contention.
 __global__ void __launch_bounds__(LC_THREADS) k_lo_count(uint32_t* __restrict__ locnt, const uint8_t* __restrict__ tlo,
                                                          const uint32_t* __restrict__ hi_off,
-                                                         const uint32_t* __restrict__ cpre, int NH, int lob) {
+                                                         const uint32_t* __restrict__ cpre,
+                                                         const uint32_t* __restrict__ bpart, int NH, int lob) {
   KGS_AUX_PRIO();
   __shared__ uint32_t cnt[SL_HIST][256];
-  __shared__ uint32_t scp[257], shi[257];
   uint32_t p, g, G, s0, s1;
-  if (!chunk_of_block_lds(cpre, hi_off, NH, blockIdx.x, scp, shi, p, g, G, s0, s1)) return;  // uniform per block
+  if (!chunk_of_block(cpre, hi_off, bpart, NH, blockIdx.x, p, g, G, s0, s1)) return;  // uniform per block
   const int nb = 1 << lob;
   const uint32_t tid = threadIdx.x;
   uint32_t c0, c1;
@@ -458,14 +486,14 @@ __device__ __forceinline__ void lo_write_runs(uint32_t* __restrict__ sorted, con
 __device__ __forceinline__ void lo_scatter_body(uint32_t* __restrict__ sorted, uint32_t* __restrict__ offsets,
                                                 const uint32_t* __restrict__ locnt, const uint32_t* __restrict__ tval,
                                                 const uint8_t* __restrict__ tlo, const uint32_t* __restrict__ hi_off,
-                                                const uint32_t* __restrict__ cpre, int NH, int lob) {
+                                                const uint32_t* __restrict__ cpre, const uint32_t* __restrict__ bpart,
+                                                int NH, int lob) {
   __shared__ uint32_t cur[256], tcnt[256], toff[256], big[256];
-  __shared__ uint32_t scp[257], shi[257];
   __shared__ uint32_t sv[SL_TILE];
   __shared__ uint32_t nbig;
   if (threadIdx.x == 0) nbig = 0;
   uint32_t p, g, G, s0, s1;
-  if (!chunk_of_block_lds(cpre, hi_off, NH, blockIdx.x, scp, shi, p, g, G, s0, s1)) return;  // uniform per block
+  if (!chunk_of_block(cpre, hi_off, bpart, NH, blockIdx.x, p, g, G, s0, s1)) return;  // uniform per block
   const uint32_t tid = threadIdx.x;
   const int nb = 1 << lob;
   // global base of each lo in this chunk: partition start + entries of smaller lo (all chunks) +
@@ -567,12 +595,13 @@ __global__ void __launch_bounds__(SL_THREADS) __attribute__((amdgpu_waves_per_eu
                                                            const uint32_t* __restrict__ tval,
                                                            const uint8_t* __restrict__ tlo,
                                                            const uint32_t* __restrict__ hi_off,
-                                                           const uint32_t* __restrict__ cpre, int NH, int lob) {
+                                                           const uint32_t* __restrict__ cpre,
+                                                           const uint32_t* __restrict__ bpart, int NH, int lob) {
   KGS_AUX_PRIO();
 #ifdef KGS_DIAG_CLOCK
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  lo_scatter_body(sorted, offsets, locnt, tval, tlo, hi_off, cpre, NH, lob);
+  lo_scatter_body(sorted, offsets, locnt, tval, tlo, hi_off, cpre, bpart, NH, lob);
 #ifdef KGS_DIAG_CLOCK
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -901,10 +930,10 @@ __global__ void __launch_bounds__(256) k_rowcol(uint32_t* __restrict__ rc, const
   const bool row = r < (1u << h);
   g1_acc29 v;
   v.set_inf();
-  const uint32_t n = row ? 1u << l : 1u << h;  // elements of this row / column (<= 256)
-  if (t < n) {
-    const uint32_t b = row ? (r << l) | t : (t << l) | (r - (1u << h));
-    if (b) v = g1_acc29::load_raw(run_rec(raw, b));
+  const uint32_t n = row ? 1u << l : 1u << h;  // elements of this row / column (up to 1024 at c = 20)
+  for (uint32_t e = t; e < n; e += 256) {       // more than 256: each thread first sums its share
+    const uint32_t b = row ? (r << l) | e : (e << l) | (r - (1u << h));
+    if (b) v.add(g1_acc29::load_raw(run_rec(raw, b)));
   }
   v = block_tree_sum(v, lds);
   if (t == 0) v.store_raw(rc + (uint64_t)RAW29_WORDS * r);
@@ -950,11 +979,11 @@ __global__ void __launch_bounds__(128) k_bitsum_rc(uint32_t* __restrict__ T, con
   if (k == c - 1) {
     if (t == 0) v = g1_acc29::load_raw(run_rec(raw, 1u << (c - 1)));
   } else {
-    const int bits = k < l ? l : h, j = k < l ? k : k - l;  // sum over 2^(bits-1) entries <= 128
+    const int bits = k < l ? l : h, j = k < l ? k : k - l;  // sum over 2^(bits-1) entries (512 at c = 20)
     const uint32_t base = k < l ? 1u << h : 0u;             // column sums follow the row sums
-    if (t < (1u << (bits - 1))) {
-      const uint32_t idx = ((t >> j) << (j + 1)) | (1u << j) | (t & ((1u << j) - 1));
-      v = g1_acc29::load_raw(rc + (uint64_t)RAW29_WORDS * (base + idx));
+    for (uint32_t e = t; e < (1u << (bits - 1)); e += 128) {
+      const uint32_t idx = ((e >> j) << (j + 1)) | (1u << j) | (e & ((1u << j) - 1));
+      v.add(g1_acc29::load_raw(rc + (uint64_t)RAW29_WORDS * (base + idx)));
     }
   }
   v = block_tree_sum(v, lds);
@@ -970,16 +999,16 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   const int c = tb.c, W = tb.W;
   const uint32_t B = 1u << (c - 1);
   // LOB bits of (key - 1) are sorted inside a partition (<= 8: tlo is a byte), the rest select one
-  // of NH = B >> LOB <= 256 partitions
-  int lob = c - 1 < 7 ? c - 1 : 7;
-  if (c - 9 > lob) lob = c - 9;
+  // of NH = B >> LOB partitions (<= 256 up to c = 17, 2^(c-9) <= NH_MAX above)
+  const int lob = msm_lob(c);
   const int NH = (int)(B >> lob);
   const uint32_t nblk = (uint32_t)((N + 256 * SORT_SPT - 1) / (256 * SORT_SPT));
-  uint32_t* ptot = w.counts;           // NH partition totals
-  uint32_t* hi_off = w.cursor;         // NH + 1
-  uint32_t* cpre = w.cursor + 300;     // NH + 1: lo-pass chunks per partition, exclusive scan
-  uint32_t* bh = w.blockhist;          // NH x nblk
-  const size_t part_lds = (size_t)256 * SORT_SPT * W * 6;
+  uint32_t* ptot = w.counts;                  // NH partition totals
+  uint32_t* hi_off = w.cursor;                // NH + 1
+  uint32_t* cpre = w.cursor + NH_MAX + 8;     // NH + 1: lo-pass chunks per partition, exclusive scan
+  uint32_t* bpart = w.cursor + 2 * (NH_MAX + 8);  // lo-pass block -> partition
+  uint32_t* bh = w.blockhist;                 // NH x nblk
+  const size_t part_lds = (size_t)256 * SORT_SPT * W * 7 + (size_t)12 * NH;
   // the scalars' standard forms (32 B each) go through w.sorted between the two sort passes: only the
   // lo pass writes it later, and it holds E = N * W >= 8 N words (W >= 9 for c <= 31)
   uint32_t* scal_std = w.sorted;
@@ -988,22 +1017,23 @@ void msm_run(hipStream_t st, const MsmTables& tb, MsmWork& w, const uint32_t* sc
   case CC:                                                                                                      \
     hipLaunchKernelGGL(k_sort_hist<CC>, dim3(nblk), dim3(256), 0, st, bh, scalars, N, lob, NH, nblk, scal_std); \
     hipLaunchKernelGGL(k_sort_scan_blocks, dim3(NH), dim3(256), 0, st, bh, ptot, nblk);                       \
-    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(64), 0, st, hi_off, ptot, NH, w.offsets, B, cpre);         \
+    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(256), 0, st, hi_off, ptot, NH, w.offsets, B, cpre, bpart); \
     hipLaunchKernelGGL(k_sort_part<CC>, dim3(nblk), dim3(256), part_lds, st, (uint32_t*)w.digit, w.lo, bh,   \
                        ptot, hi_off, scal_std, N, tb.npts, pbase, pstride, lob, NH, nblk);                    \
     break;
     KGS_SORT_C(7) KGS_SORT_C(8) KGS_SORT_C(9) KGS_SORT_C(10) KGS_SORT_C(11) KGS_SORT_C(12)
-    KGS_SORT_C(13) KGS_SORT_C(14) KGS_SORT_C(15) KGS_SORT_C(16) KGS_SORT_C(17)
+    KGS_SORT_C(13) KGS_SORT_C(14) KGS_SORT_C(15) KGS_SORT_C(16) KGS_SORT_C(17) KGS_SORT_C(18)
+    KGS_SORT_C(19) KGS_SORT_C(20)
 #undef KGS_SORT_C
     default:
-      return;  // choose_c keeps 7 <= c <= 17
+      return;  // choose_c keeps 7 <= c <= KGS_C_MAX = 20
   }
   // lo-pass grid: an upper bound of sum_p chunk_count(size_p) (blocks past cpre[NH] exit)
   const uint64_t chunk_bound = std::min<uint64_t>((uint64_t)NH * SL_G, NH + N * (uint64_t)W / SL_CHUNK);
-  hipLaunchKernelGGL(k_lo_count, dim3((unsigned)chunk_bound), dim3(LC_THREADS), 0, st, w.locnt, w.lo, hi_off, cpre, NH,
-                     lob);
+  hipLaunchKernelGGL(k_lo_count, dim3((unsigned)chunk_bound), dim3(LC_THREADS), 0, st, w.locnt, w.lo, hi_off, cpre,
+                     bpart, NH, lob);
   hipLaunchKernelGGL(k_lo_scatter, dim3((unsigned)chunk_bound), dim3(SL_THREADS), 0, st, w.sorted, w.offsets, w.locnt,
-                     (const uint32_t*)w.digit, w.lo, hi_off, cpre, NH, lob);
+                     (const uint32_t*)w.digit, w.lo, hi_off, cpre, bpart, NH, lob);
   if (ev) hipEventRecord(ev[1], st);
   const uint64_t E = N * (uint64_t)W;  // upper bound of nonzero entries
   // one segment per resident thread (KGS_ACC_WAVES blocks of 256 per CU): every accumulate

@@ -199,15 +199,21 @@ void coset_inv_prescaled(kgs_ctx& c, uint32_t* out, const uint32_t* in, int lcs)
 }
 
 // ------------------------------------------------------------------ SRS
+// Window c of the MSM tables of `npts` resident points: lg - 4, between 7 and 17. The bucket entries
+// of an N-point MSM are N * ceil(255 / c) XYZZ mixed adds, its bucket tail (row / column sums) ~2^c
+// full adds. Windows up to c = 20 are built and parity-tested (KGS_MSM_C, the sort's partitions grow
+// to 2048), but c = 20 at n = 2^20 measured slower: 13 windows instead of 15 cut the accumulation
+// 1.25 -> 1.10 ms, while the sort went 0.15 -> 0.30 ms and the tail 0.21 -> 0.53 ms, 93.3 -> 85.3
+// proofs/s in flight (DESIGN.md §13 "Wider windows", profiles/r06/wide/)
 int choose_c(uint64_t npts) {
   int lg = 0;
   while ((1ull << lg) < npts) lg++;
   int cc = lg - 4;
-  if (cc < 7) cc = 7;  // staging LDS of the partition pass: 256 * ceil(255/c) * 6 B <= 57 KB
-  if (cc > KGS_C_MAX) cc = KGS_C_MAX;
+  if (cc < 7) cc = 7;  // staging LDS of the partition pass: 256 * 2 * ceil(255/c) * 7 B <= 133 KB
+  if (cc > 17) cc = 17;
   if (const char* e = getenv("KGS_MSM_C")) {  // A/B override of the window
     int v = atoi(e);
-    if (v >= 7 && v <= 17) cc = v;
+    if (v >= 7 && v <= KGS_C_MAX) cc = v;
   }
   return cc;
 }
@@ -229,12 +235,15 @@ void ensure_msm_work(kgs_ctx& c) {
     w.digit = (int32_t*)c.buf("msm_digit" + sfx, E * 4);
     w.sorted = c.buf("msm_sorted" + sfx, E * 4);
     w.lo = (uint8_t*)c.buf("msm_lo" + sfx, E);
-    w.blockhist = c.buf("msm_blockhist" + sfx, 4 * 264 * ((npts + 255) / 256 + 1));
-    w.counts = c.buf("msm_counts" + sfx, 4 * (B + 300));
+    const size_t NH = (size_t)msm_nh(cc);
+    w.blockhist = c.buf("msm_blockhist" + sfx, 4 * (NH + 8) * ((npts + 255) / 256 + 1));
+    w.counts = c.buf("msm_counts" + sfx, 4 * (NH + 300));
     w.offsets = c.buf("msm_offsets" + sfx, 4 * (B + 4));
-    w.cursor = c.buf("msm_cursor" + sfx, 4 * (B + 600));
+    // hi_off (NH + 1), cpre (NH + 1) at MSM_NH_MAX + 8 words each, then the lo pass's block ->
+    // partition table (at most NH + E / 16384 chunks: msm.hip chunk_bound)
+    w.cursor = c.buf("msm_cursor" + sfx, 4 * (2 * ((size_t)MSM_NH_MAX + 8) + NH + E / 16384 + 64));
     w.segowner = c.buf("msm_segowner" + sfx, 4 * nseg);
-    w.locnt = c.buf("msm_locnt" + sfx, 4 * 256 * 256 * (size_t)MSM_SL_G_MAX);  // partitions x lo x chunks
+    w.locnt = c.buf("msm_locnt" + sfx, 4 * NH * 256 * (size_t)MSM_SL_G_MAX);  // partitions x lo x chunks
     w.chunklist = c.buf("msm_chunklist" + sfx, 4 * 3 * (nseg / 16 + B + 16));
     w.chunkcnt = c.buf("msm_chunkcnt" + sfx, 64);
     w.raw29 = c.buf("msm_raw29" + sfx, 160 * ((size_t)B + 2 + nseg));

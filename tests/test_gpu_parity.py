@@ -257,6 +257,36 @@ def test_msm_skewed_multitile_linearity(K):
     ctx.close()
 
 
+@pytest.mark.parametrize("c", [18, 19, 20])
+def test_msm_wide_windows(K, monkeypatch, c):
+    """Windows wider than the default 17 (KGS_MSM_C; 512 / 1024 / 2048 sort partitions, a 2^17-2^19
+    bucket tail): MSMs of random, degenerate and skewed scalars against oracle/c, and a proof
+    byte-identical to the C restatement. A ptau file of its own keeps these tables from being shared
+    with the default-window contexts."""
+    from oracle import cbackend as C
+    monkeypatch.setenv("KGS_MSM_C", str(c))
+    nbits = 12
+    path = f"/tmp/kgs_test_gpu_wide{c}.{os.getpid()}.ptau"
+    try:
+        ctx = K.Context(0)
+        ctx.write_synthetic_ptau(path, nbits, common.tau())
+        ctx.load_ptau(path, nbits)
+        assert ctx.srs_info()[2] == c
+        _, sb = C.load_srs_bytes(path)
+        rnd = random.Random(c)
+        n = 1 << nbits
+        for v in (rv(rnd, 1), rv(rnd, 777), rv(rnd, n), [7] * n, [R - 1] * 33, [0] * 9 + [5]):
+            mb = common.mont_bytes(v)
+            assert ctx.msm(mb) == C.msm(sb, mb), len(v)
+        Fs, Ts, sF, sT = common.make_inputs(3000 + c, 11, 2, True)
+        got = ctx.prove(K.GRANDSUM, 11, Fs, Ts, sF, sT, mont_out=False)[:2]
+        assert got == tuple(C.prove_raw(K.GRANDSUM, 11, Fs, Ts, sF, sT, sb, 0))
+        ctx.close()
+    finally:
+        if os.path.exists(path):
+            os.remove(path)
+
+
 @pytest.mark.parametrize("kind", [0, 1])
 @pytest.mark.parametrize("sel", [False, True])
 @pytest.mark.parametrize("nbits", [1, 4, 11, 13])
