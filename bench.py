@@ -470,13 +470,25 @@ def main():
     value = total_proofs / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
     log(f"timed: {value:.2f} proofs/s device-resident; host-buffer in flight")
-    el_host = timed(run_host, "kgs_bench_host_region")
+    # the host-buffer path in flight: three regions of the same K steps, interleaved with two more
+    # device-resident ones, so the ratio compares medians of neighbouring runs (a single pair of runs
+    # spread 0.95-0.99 on one box, profiles/r06/host_inflight_modes.txt); `value` stays the first region
+    el_hosts, el_devs = [], [elapsed]
+    for i in range(3):
+        el_hosts.append(timed(run_host, "kgs_bench_host_region"))
+        if i < 2:
+            el_devs.append(timed(run_dev, "kgs_bench_timed_region_extra"))
+    el_host = float(np.median(el_hosts))
     host_inflight = {
         "proofs_per_s": round(total_proofs / el_host, 4), "ms_per_step": round(1000.0 * el_host / args.steps, 3),
-        "vs_device_resident": round(el_host and (total_proofs / el_host) / value, 4),
+        "vs_device_resident": round(float(np.median(el_devs)) / el_host, 4),
+        "samples_proofs_per_s": [round(total_proofs / x, 3) for x in el_hosts],
+        "device_samples_proofs_per_s": [round(total_proofs / x, 3) for x in el_devs],
         "proof_identical_to_device_path": host_identical,
         "note": (f"kgs_prove on pageable host F/T, {len(ctxs)} contexts in flight, Montgomery forms written back into "
-                 "caller-owned host buffers (prover.js:147-148): PCIe-inclusive, same steps as `value`")}
+                 "caller-owned host buffers (prover.js:147-148): PCIe-inclusive, K steps per region like `value`; "
+                 "median of 3 regions, ratio against the median of 3 device-resident regions (the first is `value`) "
+                 "run interleaved")}
 
     # ---------------- host-buffer boundary latency (what the JS / Python drop-in modules call): kgs_prove
     # on pageable host buffers, including the H2D copy of F/T and the D2H Montgomery write-back
@@ -537,9 +549,10 @@ def main():
         msm_ms = sum(ph)
         W = (255 + window_c - 1) // window_c
         B = 1 << (window_c - 1)
-        # executed G1 additions: one mixed add per (bucket, point) entry + combine (~ segments) +
-        # bit-sum trees (~ c * B / 2) + host Horner (2c)
-        adds_exec = entries.value + window_c * (B // 2) + 2 * window_c
+        # executed G1 additions: one mixed add per (bucket, point) entry + the bucket tail's row and
+        # column sums (2B) and bit sums (c * 2^(l-1), l = c // 2; msm.hip k_rowcol / k_bitsum_rc) + host
+        # Horner (2c); the combine of segment partials (~ segments) is left out
+        adds_exec = entries.value + 2 * B + window_c * (1 << (window_c // 2 - 1)) + 2 * window_c
         msm = {
             "n_points": n, "window_c": window_c, "windows": W, "precomputed_windows": True,
             "ms": round(msm_ms, 4), "phase_ms": {"digits_sort": round(ph[0], 4), "accumulate": round(ph[1], 4),

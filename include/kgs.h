@@ -160,7 +160,12 @@ int kgs_ctx_set_msm_lanes(kgs_ctx_t* ctx, int lanes);
  * rank group (kgs_ctx_set_group) decides the degenerate cases from all-gathered degrees and replays
  * the chain on the gathered operands on every rank: every rank fails with the reference's error, or
  * returns the reference's proof. The replay reproduces transforms of up to 2^26 points (the
- * reference's own need n^2 points for a degree-1 operand); beyond that it fails with KGS_E_ARG. */
+ * reference's own need n^2 points for a degree-1 operand); beyond that it fails with KGS_E_ARG.
+ * One gap remains in rank groups: a replay that writes into polF's buffer (the unselected grand-sum's
+ * polQ1.add(polF) on a shorter polQ1) makes a group fail with KGS_E_ARG where the
+ * single-GPU prover follows the reference. No valid multiset of the test families reaches it with a
+ * proof: the oracle restatement hits that write only on zero quotients (F == T), where the replay
+ * first throws the reference's RangeError (DESIGN.md §13 "Q2 in rank groups"). */
 int kgs_ctx_set_reference_quirks(kgs_ctx_t* ctx, int on);
 
 /* Load a .ptau file (binfileutils layout, sections 1-3) and make the first 2^(nbits_max+1) G1

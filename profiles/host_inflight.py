@@ -63,11 +63,25 @@ def main():
     for mode in modes:
         for m in counts:
             go(mode, m, 2 * m)  # warm
+    def cpu_stat():  # the box's cgroup CPU accounting (quota throttling), when readable
+        try:
+            with open("/sys/fs/cgroup/cpu.stat") as fh:
+                return {k: int(v) for k, v in (ln.split() for ln in fh if ln.strip())}
+        except Exception:
+            return None
+
     for r in range(reps):
         for m in counts:
             for mode in modes:
+                s0 = cpu_stat()
                 el = go(mode, m, steps)
-                print(f"rep {r} {mode:8s} contexts {m}: {steps / el:7.2f} proofs/s", flush=True)
+                s1 = cpu_stat()
+                extra = ""
+                if s0 and s1:
+                    d = {k: s1[k] - s0.get(k, 0) for k in ("usage_usec", "nr_throttled", "throttled_usec") if k in s1}
+                    extra = (f" | cpu {d.get('usage_usec', 0) / 1e3 / el / 1e3:5.2f} cores, throttled "
+                             f"{d.get('nr_throttled', 0)} periods {d.get('throttled_usec', 0) / 1e3:.1f} ms")
+                print(f"rep {r} {mode:8s} contexts {m}: {steps / el:7.2f} proofs/s{extra}", flush=True)
 
 
 if __name__ == "__main__":
