@@ -157,6 +157,22 @@ def test_c4_grandsum_2p24(K):
     c4_single(K)
 
 
+@pytest.mark.skipif(not os.environ.get("KGS_TEST_EXACT_2P24"), reason="opt-in (KGS_TEST_EXACT_2P24=1): ~2 min of "
+                    "oracle/c on 16 cores; run once per round, result in profiles/r06/exact_2p24.log")
+@pytest.mark.timeout(1200)
+def test_c4_grandsum_2p24_exact(K):
+    """configs[3] byte for byte against oracle/c's prove_raw (same inputs and SRS as c4_single)."""
+    from oracle import cbackend as C
+    want = c4_single(K)
+    nbits = 24
+    Fs, Ts, sF, sT = np_inputs(0xC4, nbits, 1, False)
+    _, srs = C.load_srs_bytes(gpu_ptau(K, nbits))
+    ecoms, eevs = C.prove_raw(0, nbits, Fs, Ts, sF, sT, srs, 0)
+    cn, en = K.proof_names(K.GRANDSUM, 1, False)
+    assert [want["commitments"][c] for c in cn] == ecoms
+    assert [want["evaluations"][e] for e in en] == eevs
+
+
 def test_c4_msm_sharded_2p24_w8(K):
     """configs[3]'s MSM point-range split at its own size: n = 2^24 over 8 simulated ranks on cuda:0
     (polynomial.js:1106-1115 split by point range); every rank == the one-GPU proof, byte for byte"""
