@@ -94,8 +94,8 @@ static void build_twin(kgs_ctx& c, DomainTables* d) {
   ntt_register_tw29(d->mem, entries, d->mem29);
 }
 void ensure_twin(kgs_ctx& c) {
-  if (!c.dom || c.dom->mem29) return;
-  std::lock_guard<std::mutex> lk(g_reg_mu);
+  if (!c.dom) return;
+  std::lock_guard<std::mutex> lk(g_reg_mu);  // mem29 is written under this lock (by any context)
   build_twin(c, c.dom.get());
 }
 
