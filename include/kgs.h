@@ -297,6 +297,13 @@ int kgs_bench_msm_phases(kgs_ctx_t* ctx, const void* d_scalars_mont, uint64_t n,
                          uint64_t* entries);
 /* Run `reps` forward+inverse NTT pairs of size 2^logm on a device buffer; returns ms. */
 int kgs_bench_ntt(kgs_ctx_t* ctx, void* d_buf, int logm, int reps, double* ms);
+/* Host-only test hook of kgs_prove's staging copy (no GPU): copies len bytes src -> dst the way a
+ * host input vector is staged (256 KiB pieces over the copy pool, spans of `span` bytes reported in
+ * order once copied). spans_out[i] receives the byte offset of the i-th reported span (up to max);
+ * fail_at >= 0 makes the report of span fail_at fail, the way a failed DMA enqueue does: the copy
+ * then still completes and the call returns KGS_E_HIP. *nspans = spans reported. */
+int kgs_test_stream_copy(uint8_t* dst, const uint8_t* src, uint64_t len, uint64_t span, int fail_at,
+                         uint64_t* spans_out, int max, int* nspans);
 
 #ifdef __cplusplus
 }

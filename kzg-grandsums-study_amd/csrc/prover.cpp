@@ -1701,6 +1701,19 @@ int kgs_host_unregister(void* ptr) {
   API_END
 }
 
+int kgs_test_stream_copy(uint8_t* dst, const uint8_t* src, uint64_t len, uint64_t span, int fail_at,
+                         uint64_t* spans_out, int max, int* nspans) {
+  API_BEGIN
+  if (!dst || !src || !nspans || (max > 0 && !spans_out)) throw KgsError(KGS_E_ARG, "NULL argument");
+  *nspans = 0;
+  stream_copy(dst, src, (size_t)len, (size_t)span, [&](size_t o, size_t) {
+    if (*nspans == fail_at) throw KgsError(KGS_E_HIP, "injected span failure");
+    if (*nspans < max) spans_out[*nspans] = o;
+    (*nspans)++;
+  });
+  API_END
+}
+
 int kgs_ctx_idle(kgs_ctx_t* ctx) {
   API_BEGIN
   if (!ctx) throw KgsError(KGS_E_ARG, "NULL ctx");

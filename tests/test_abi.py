@@ -63,3 +63,42 @@ def test_python_mirror_names():
     com, ev = K.proof_names(K.GRANDPRODUCT, 2, True)
     assert com == ["F0", "T0", "F1", "T1", "selF", "selT", "Z", "Q", "Wxi", "Wxiw"]
     assert ev == ["f0xi", "f1xi", "selFxi", "selTxi", "zxiw"]
+
+
+@pytest.mark.parametrize("length,span", [(1, 2 << 20), (1000, 2 << 20), (32 << 20, 2 << 20), ((32 << 20) + 77, 8 << 20),
+                                         (3 << 20, 256 << 10), (5 << 20, 100)])
+def test_stream_copy_spans_in_order(lib, length, span):
+    """kgs_prove's staging copy (prover.cpp stream_copy, host only): every byte copied, every DMA span
+    reported once, in address order, each only after all of its bytes were written."""
+    import numpy as np
+    rng = np.random.default_rng(length)
+    src = rng.integers(0, 256, size=length, dtype=np.uint8)
+    dst = np.zeros(length, dtype=np.uint8)
+    span_eff = max(256 << 10, span // (256 << 10) * (256 << 10))
+    nmax = (length + span_eff - 1) // span_eff
+    spans = (ctypes.c_uint64 * max(nmax, 1))()
+    n = ctypes.c_int()
+    rc = lib.kgs_test_stream_copy(ctypes.c_void_p(dst.ctypes.data), ctypes.c_void_p(src.ctypes.data),
+                                  ctypes.c_uint64(length), ctypes.c_uint64(span), -1, spans, nmax, ctypes.byref(n))
+    assert rc == 0
+    assert np.array_equal(dst, src)
+    assert n.value == nmax
+    assert list(spans)[:nmax] == [i * span_eff for i in range(nmax)]
+
+
+def test_stream_copy_failed_span_still_completes(lib):
+    """A span whose DMA enqueue fails: the error is returned only after every piece is copied (the
+    pool's helpers never write into the staging after the call), and no later span is reported."""
+    import numpy as np
+    length = 24 << 20
+    src = np.arange(length, dtype=np.uint64).astype(np.uint8)
+    dst = np.zeros(length, dtype=np.uint8)
+    spans = (ctypes.c_uint64 * 16)()
+    n = ctypes.c_int()
+    rc = lib.kgs_test_stream_copy(ctypes.c_void_p(dst.ctypes.data), ctypes.c_void_p(src.ctypes.data),
+                                  ctypes.c_uint64(length), ctypes.c_uint64(2 << 20), 3, spans, 16, ctypes.byref(n))
+    assert rc != 0
+    lib.kgs_last_error.restype = ctypes.c_char_p
+    assert b"injected span failure" in lib.kgs_last_error()
+    assert n.value == 3  # spans 0, 1, 2 reported; the failing one and the rest not
+    assert np.array_equal(dst, src)
