@@ -1418,15 +1418,20 @@ static unsigned copy_threads() {
   return n;
 }
 namespace {
-// 16 B non-temporal stores: the staging copy writes 32 MiB that the CPU never reads back, so the
-// stores bypass the caches (no read-for-ownership of the destination lines). Measured on the GPU
-// box's host (profiles/ubench/host_copy_bw.cpp, profiles/r06/host_copy_bw.txt): one 32 MiB vector
-// into pinned staging in 0.26 ms with 4 threads (130 GB/s) against 0.44 ms for memcpy. The sfence
-// makes the lines globally visible before the piece is counted done, i.e. before its DMA is enqueued.
+// The staging copy's stores. Default: memcpy (cached stores). KGS_COPY_NT=1: 16 B non-temporal
+// stores, which bypass the caches and copy a 32 MiB vector into pinned staging in 0.26 ms with 4
+// threads against 0.44 ms for memcpy (profiles/ubench/host_copy_bw.cpp, profiles/r06/host_copy_bw.txt),
+// but the proof is slower with them: the H2D DMA then reads the staging from DRAM instead of the host's
+// L3 (512 MB on the GPU box), and F's DMA, not its copy, is what the proof waits for. JS single-proof
+// median, same box, 4 x 15 samples: 15.1-16.1 ms with memcpy, 16.8-17.8 with NT stores
+// (profiles/r06/js_lat_ab.txt); again 15.7-16.6 vs 16.9-17.9 on another box, where the Python host
+// call went the other way (14.7-15.1 vs 14.4-14.6 ms; profiles/r06/copy_final_ab/). The JavaScript
+// module is the drop-in, so its median decides. With NT stores the sfence makes the lines globally
+// visible before the piece is counted done, i.e. before its DMA is enqueued.
 void copy_nt(uint8_t* d, const uint8_t* s, size_t n) {
-  static const bool plain = [] {  // KGS_COPY_NT=0: memcpy (A/B)
+  static const bool plain = [] {  // KGS_COPY_NT=1: non-temporal stores (A/B)
     const char* e = getenv("KGS_COPY_NT");
-    return e && e[0] == '0';
+    return !(e && e[0] == '1');
   }();
   if (plain) {
     memcpy(d, s, n);
