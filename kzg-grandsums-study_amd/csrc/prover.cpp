@@ -1418,22 +1418,27 @@ static unsigned copy_threads() {
   return n;
 }
 namespace {
-// The staging copy's stores. Default: memcpy (cached stores). KGS_COPY_NT=1: 16 B non-temporal
-// stores, which bypass the caches and copy a 32 MiB vector into pinned staging in 0.26 ms with 4
-// threads against 0.44 ms for memcpy (profiles/ubench/host_copy_bw.cpp, profiles/r06/host_copy_bw.txt),
-// but the proof is slower with them: the H2D DMA then reads the staging from DRAM instead of the host's
-// L3 (512 MB on the GPU box), and F's DMA, not its copy, is what the proof waits for. JS single-proof
-// median, same box, 4 x 15 samples: 15.1-16.1 ms with memcpy, 16.8-17.8 with NT stores
-// (profiles/r06/js_lat_ab.txt); again 15.7-16.6 vs 16.9-17.9 on another box, where the Python host
-// call went the other way (14.7-15.1 vs 14.4-14.6 ms; profiles/r06/copy_final_ab/). The JavaScript
-// module is the drop-in, so its median decides. With NT stores the sfence makes the lines globally
-// visible before the piece is counted done, i.e. before its DMA is enqueued.
-void copy_nt(uint8_t* d, const uint8_t* s, size_t n) {
-  static const bool plain = [] {  // KGS_COPY_NT=1: non-temporal stores (A/B)
+// The staging copy's stores: cached (memcpy) or 16 B non-temporal. NT stores bypass the caches and
+// copy a 32 MiB vector into pinned staging in 0.26 ms with 4 threads against 0.44 ms for memcpy
+// (profiles/ubench/host_copy_bw.cpp, profiles/r06/host_copy_bw.txt), but then the H2D DMA reads the
+// staging from DRAM instead of the host's L3, and F's DMA, not its copy, is what a lone proof waits
+// for. Measured (same boxes, interleaved): a lone proof through the JavaScript module is faster with
+// cached stores, median 15.1-16.1 vs 16.8-17.8 ms (4 x 15 samples, profiles/r06/js_lat_ab.txt; again
+// 15.7-16.6 vs 16.9-17.9, profiles/r06/copy_final_ab/). Four proofs in flight are faster with NT
+// stores, 0.9727 vs 0.9664 of device-resident (12 samples each, profiles/r06/inflight_store_ab/). So by
+// default (KGS_COPY_NT unset) a copy uses NT stores when another proof of the process is in progress,
+// cached stores when its proof is alone; KGS_COPY_NT=0 / 1 forces one kind. With NT stores the sfence
+// makes the lines globally visible before the piece is counted done, i.e. before its DMA is enqueued.
+std::atomic<int> g_proofs_active{0};  // kgs_prove calls in progress in the process
+bool copy_nt_now() {
+  static const int mode = [] {
     const char* e = getenv("KGS_COPY_NT");
-    return !(e && e[0] == '1');
+    return e && e[0] == '1' ? 1 : e && e[0] == '0' ? 0 : -1;
   }();
-  if (plain) {
+  return mode == 1 || (mode < 0 && g_proofs_active.load(std::memory_order_relaxed) > 1);
+}
+void copy_stores(uint8_t* d, const uint8_t* s, size_t n, bool nt) {
+  if (!nt) {
     memcpy(d, s, n);
     return;
   }
@@ -1467,6 +1472,7 @@ struct CopyTask {
   // stream_copy: pieces left to copy per DMA piece (piece i belongs to DMA piece i / per_dma)
   std::unique_ptr<std::atomic<uint32_t>[]> left;
   size_t per_dma = 0;
+  bool nt = false;  // non-temporal stores (decided once per copy: copy_nt_now)
   std::mutex mu;
   std::condition_variable cv;
   bool copy_one(size_t i) {  // false: nothing left to claim
@@ -1475,7 +1481,7 @@ struct CopyTask {
       fprintf(stderr, "kgs: copy piece %zu claimed after its task completed\n", i);
       abort();
     }
-    copy_nt(pieces[i].dst, pieces[i].src, pieces[i].len);
+    copy_stores(pieces[i].dst, pieces[i].src, pieces[i].len, nt);
     if (left) left[i / per_dma].fetch_sub(1, std::memory_order_release);
     return true;
   }
@@ -1546,6 +1552,7 @@ void start_helpers(const std::shared_ptr<CopyTask>& task, unsigned nth) {
 void par_copy(const std::vector<CopyJob>& jobs) {
   const size_t piece = 1u << 20;
   auto task = std::make_shared<CopyTask>();
+  task->nt = copy_nt_now();
   for (const auto& j : jobs)
     for (size_t o = 0; o < j.len; o += piece) task->pieces.push_back({j.dst + o, j.src + o, std::min(piece, j.len - o)});
   Active active;
@@ -1567,6 +1574,7 @@ void stream_copy(uint8_t* dst, const uint8_t* src, size_t len, size_t dma, const
   const size_t sub = (size_t)256 << 10;
   dma = std::max(sub, dma / sub * sub);
   auto task = std::make_shared<CopyTask>();
+  task->nt = copy_nt_now();
   for (size_t o = 0; o < len; o += sub) task->pieces.push_back({dst + o, src + o, std::min(sub, len - o)});
   const size_t ndma = (len + dma - 1) / dma;
   task->per_dma = dma / sub;
@@ -1747,6 +1755,10 @@ int kgs_prove(kgs_ctx_t* ctx, int kind, int nbits, int npols, const uint8_t* con
   // error return drains the context's streams, so no DMA of this call still reads or writes caller
   // memory (pinned inputs DMA'd in place, pinned write-back targets) once the caller has it back
   DrainOnError drain(ctx);
+  struct ProofActive {  // kgs_prove calls in progress (the staging copy's store choice, copy_nt_now)
+    ProofActive() { g_proofs_active.fetch_add(1, std::memory_order_relaxed); }
+    ~ProofActive() { g_proofs_active.fetch_sub(1, std::memory_order_relaxed); }
+  } proof_active;
   const uint64_t n = 1ull << nbits;
   const size_t E = 32 * n;
   ProveIn in;
