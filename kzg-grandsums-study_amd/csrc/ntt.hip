@@ -530,12 +530,14 @@ __device__ __forceinline__ void lds_round_all(uint32_t* lds, const uint32_t* __r
 #define KGS_NTT_PF3 0
 #endif
 // T29: the twiddle products in 9 x 29-bit limbs (tw = the domain's 29-bit twin table, fr29.hpp)
-template <int K1, int K2, int K3, bool DIT, bool DIRECT, int WV, bool T29>
+// K4 > 0 (2^12-element tiles only, -DKGS_NTT_ELOG=12): a fourth register round, up to 12 stages per pass
+template <int K1, int K2, int K3, int K4, bool DIT, bool DIRECT, int WV, bool T29>
 __global__ void __launch_bounds__(LDS_NT) __attribute__((amdgpu_waves_per_eu(WV, WV)))
 k_ntt_lds_pass(ntt_io io, const uint32_t* __restrict__ tw, int s0) {
   using TW = typename std::conditional<T29, W29, fr>::type;
   KGS_AUX_PRIO();
-  constexpr int K = K1 + K2 + K3;
+  constexpr int K = K1 + K2 + K3 + K4;
+  static_assert(K4 == 0 || K3 > 0, "rounds are filled in order");
   constexpr int LBLOG = NTT_ELOG - K;
   constexpr int LB = 1 << LBLOG;
   uint32_t* lds;
@@ -558,11 +560,17 @@ k_ntt_lds_pass(ntt_io io, const uint32_t* __restrict__ tw, int s0) {
     }
     __syncthreads();
   }
-  // DIF: bits [K-K1, K), [K-K1-K2, K-K1), [0, K3); DIT: [0, K1), [K1, K1+K2), [K1+K2, K)
+  // DIF: bits [K-K1, K), [K-K1-K2, K-K1), ... down to 0; DIT: [0, K1), [K1, K1+K2), ... up to K
   constexpr bool PF = WV < 3 || KGS_NTT_PF3;
   lds_round_all<K1, DIT, DIRECT, false, PF, TW>(lds, tw, io, col0, K, logd, LBLOG, DIT ? 0 : K - K1);
   __syncthreads();
-  if constexpr (K3 > 0) {
+  if constexpr (K4 > 0) {
+    lds_round_all<K2, DIT, false, false, PF, TW>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 : K3 + K4);
+    __syncthreads();
+    lds_round_all<K3, DIT, false, false, PF, TW>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 + K2 : K4);
+    __syncthreads();
+    lds_round_all<K4, DIT, false, DIRECT, PF, TW>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 + K2 + K3 : 0);
+  } else if constexpr (K3 > 0) {
     lds_round_all<K2, DIT, false, false, PF, TW>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 : K3);
     __syncthreads();
     lds_round_all<K3, DIT, false, DIRECT, PF, TW>(lds, tw, io, col0, K, logd, LBLOG, DIT ? K1 + K2 : 0);
@@ -648,7 +656,28 @@ constexpr int LDS_MAX_K = NTT_ELOG - 2 < 9 ? NTT_ELOG - 2 : 9;  // >= 4 columns 
 // to 9 stages (three register rounds), the others 6 (two rounds, 1 KiB runs) unless more are needed.
 // 2^20 = 6+6+8, 2^21 = 6+6+9, 2^22 = 7+6+9, 2^24 = 8+7+9: three passes where the radix-8 tail pass
 // made four.
+//
+// 2^12-element tiles (-DKGS_NTT_ELOG=12: 128 KiB of LDS, 512 threads, one block per CU): the
+// contiguous pass takes up to 12 stages (four register rounds), the others up to 10 (>= 4 columns per
+// tile): 2^20 = 8+12, 2^21 = 9+12, 2^22 = 10+12, 2^24 = 6+6+12, i.e. one global round trip fewer.
 static int lds_plan(int logm, int* ks) {
+  if (NTT_ELOG >= 12) {
+    int E = logm < NTT_ELOG ? logm : NTT_ELOG;
+    int rest = logm - E;
+    if (rest > 0 && rest < 4) {  // passes of >= 4 stages (two register rounds of >= 2)
+      E = logm - 4;
+      rest = 4;
+    }
+    const int maxk = NTT_ELOG - 2;
+    const int P = 1 + (rest + maxk - 1) / maxk;
+    for (int i = 0; i < P - 1; i++) {
+      const int left = P - 1 - i;
+      ks[i] = (rest + left - 1) / left;
+      rest -= ks[i];
+    }
+    ks[P - 1] = E;
+    return P;
+  }
   const int P = (logm + LDS_MAX_K - 1) / LDS_MAX_K;
   int E = logm - 6 * (P - 1);
   if (E > LDS_MAX_K) E = LDS_MAX_K;
@@ -675,30 +704,43 @@ static void launch_lds_pass(hipStream_t st, int K, bool dit, uint32_t* data, con
   const ntt_io io{data, in, in_len, in_bitrev, pre, post, post_s, logm, pre29, post29, post_s29};
   const int logd = dit ? s0 : logm - s0 - K;
   static const bool staged = getenv("KGS_NTT_STAGED") != nullptr;  // A/B: every pass staged through LDS
-  const bool direct = logd >= NTT_ELOG - K && !staged;
-#define KGS_LDS_LAUNCH2(A, B, C, D, E, T, TWP)                                                                 \
+  // A/B: a whole-tile pass (K = NTT_ELOG, one column of consecutive elements) loads and stores its
+  // rounds directly as well (lanes then step 1 or 2^R elements)
+  static const bool direct_tile = getenv("KGS_NTT_DIRECT_TILE") != nullptr;
+  const bool direct = logd >= NTT_ELOG - K && (NTT_ELOG - K >= 2 || direct_tile) && !staged;
+#define KGS_LDS_LAUNCH2(A, B, C, F, D, E, T, TWP)                                                              \
   do {                                                                                                         \
     if (g_ntt_coresident)                                                                                      \
-      hipLaunchKernelGGL((k_ntt_lds_pass<A, B, C, D, E, 3, T>), dim3(blocks), dim3(LDS_NT), LDS_ELEMS * 32, st, \
-                         io, TWP, s0);                                                                         \
+      hipLaunchKernelGGL((k_ntt_lds_pass<A, B, C, F, D, E, 3, T>), dim3(blocks), dim3(LDS_NT), LDS_ELEMS * 32,  \
+                         st, io, TWP, s0);                                                                     \
     else                                                                                                       \
-      hipLaunchKernelGGL((k_ntt_lds_pass<A, B, C, D, E, 2, T>), dim3(blocks), dim3(LDS_NT), 0, st, io, TWP, s0); \
+      hipLaunchKernelGGL((k_ntt_lds_pass<A, B, C, F, D, E, 2, T>), dim3(blocks), dim3(LDS_NT), 0, st, io, TWP, \
+                         s0);                                                                                  \
   } while (0)
-#define KGS_LDS_LAUNCH(A, B, C, D, E)             \
-  do {                                            \
-    if (tw29)                                     \
-      KGS_LDS_LAUNCH2(A, B, C, D, E, true, tw29); \
-    else                                          \
-      KGS_LDS_LAUNCH2(A, B, C, D, E, false, tw);  \
+#define KGS_LDS_LAUNCH(A, B, C, F, D, E)             \
+  do {                                               \
+    if (tw29)                                        \
+      KGS_LDS_LAUNCH2(A, B, C, F, D, E, true, tw29); \
+    else                                             \
+      KGS_LDS_LAUNCH2(A, B, C, F, D, E, false, tw);  \
   } while (0)
-#define KGS_LDS_BY_K(D, E)                          \
-  switch (K) {                                      \
-    case 9: KGS_LDS_LAUNCH(3, 3, 3, D, E); break;   \
-    case 8: KGS_LDS_LAUNCH(3, 3, 2, D, E); break;   \
-    case 7: KGS_LDS_LAUNCH(3, 2, 2, D, E); break;   \
-    case 6: KGS_LDS_LAUNCH(3, 3, 0, D, E); break;   \
-    case 5: KGS_LDS_LAUNCH(3, 2, 0, D, E); break;   \
-    default: KGS_LDS_LAUNCH(2, 2, 0, D, E); break;  \
+#if KGS_NTT_ELOG >= 12
+#define KGS_LDS_BY_K_WIDE(D, E)                          \
+  case 12: KGS_LDS_LAUNCH(3, 3, 3, 3, D, E); break;      \
+  case 11: KGS_LDS_LAUNCH(3, 3, 3, 2, D, E); break;      \
+  case 10: KGS_LDS_LAUNCH(3, 3, 2, 2, D, E); break;
+#else
+#define KGS_LDS_BY_K_WIDE(D, E)
+#endif
+#define KGS_LDS_BY_K(D, E)                             \
+  switch (K) {                                         \
+    KGS_LDS_BY_K_WIDE(D, E)                            \
+    case 9: KGS_LDS_LAUNCH(3, 3, 3, 0, D, E); break;   \
+    case 8: KGS_LDS_LAUNCH(3, 3, 2, 0, D, E); break;   \
+    case 7: KGS_LDS_LAUNCH(3, 2, 2, 0, D, E); break;   \
+    case 6: KGS_LDS_LAUNCH(3, 3, 0, 0, D, E); break;   \
+    case 5: KGS_LDS_LAUNCH(3, 2, 0, 0, D, E); break;   \
+    default: KGS_LDS_LAUNCH(2, 2, 0, 0, D, E); break;  \
   }
   if (dit) {
     if (direct) {
@@ -714,6 +756,7 @@ static void launch_lds_pass(hipStream_t st, int K, bool dit, uint32_t* data, con
     }
   }
 #undef KGS_LDS_BY_K
+#undef KGS_LDS_BY_K_WIDE
 #undef KGS_LDS_LAUNCH
 #undef KGS_LDS_LAUNCH2
 }
