@@ -107,6 +107,9 @@ void ensure_domain(kgs_ctx& c, int logM, bool twin) {
     auto d = w.lock();
     if (d && d->device == c.device && d->logM >= logM) {
       if (twin) build_twin(c, d.get());
+      // switching may drop the last reference to the old tables (freed at once): nothing of this
+      // context may still read them. Every caller drains its streams first today; this keeps it so.
+      c.sync();
       c.use_domain(d);
       c.nxm1.clear();
       return;
