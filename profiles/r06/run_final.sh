@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/../.."
 R=$PWD
-OUT=$R/gpurun_out/r06/final
+OUT=$R/gpurun_out/r06/${FINAL_DIR:-final}
 mkdir -p $OUT
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 1100 python3 -u -m pytest tests/ -m gpu -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { grep -E "FAILED|Error" $OUT/gpu_tests.log | head -30; tail -5 $OUT/gpu_tests.log; exit 1; }
