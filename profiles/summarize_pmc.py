@@ -2,11 +2,9 @@
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (run separately, per the MI355X guide)
 into profiles/pmc_<round>.json and profiles/pmc_accumulate.json (read by bench.py's roofline).
 
-Counters are in KB per dispatch. The gfx950 FETCH_SIZE correction (x2) is calibrated for wide
-coalesced 16 B/lane streaming reads; k_accumulate's reads are random 64 B point records (4 x 16 B
-per lane, one record per lane), i.e. a different pattern, so both the raw and the x2-corrected
-figures are recorded and the RAW one is used as `traffic` (it already exceeds the algorithmic
-bytes ~1.9x: each 64 B record pulls a 128 B line).
+Counters are in KB per dispatch. Both the raw FETCH_SIZE and the gfx950-corrected (x2) figure are
+recorded; since round 6 bench.py reports the corrected one as `roofline.traffic` (the MI355X
+guide's HBM recipe) with the raw one beside it.
 usage: summarize_pmc.py <pmc_FETCH_SIZE dir> <pmc_WRITE_SIZE dir> <round tag>
 (both passes over `python3 profiles/msm_loop.py 20 3`)
 """
