@@ -768,7 +768,9 @@ void prove_impl(kgs_ctx& c, const ProveIn& in, uint8_t* com_out, uint8_t* ev_out
     HC(hipEventRecord(c.ev_wb[nwb], st));
     HC(hipStreamWaitEvent(c.st_wb, c.ev_wb[nwb], 0));
     nwb++;
-    // hipMemcpyAsync (an SDMA engine: no CU time). KGS_WB_COPY=kernel stores from a shader into the
+    // hipMemcpyAsync. Into pinned memory the runtime runs it as its copyBuffer shader kernel, not on an
+    // SDMA engine: ~0.8 ms of CU residency per 32 MiB in flight; hipMemcpyDtoHAsync does the same
+    // (profiles/r06/host_engine/, wb_api/). KGS_WB_COPY=kernel stores from our own shader into the
     // mapped pinned buffer instead (poly.hip k_host_store): measured slower in flight, 83-85 vs 86-88
     // proofs/s (profiles/r05/wb_ab.txt), kept for A/B
     static const unsigned wb_blocks = [] {
